@@ -1,0 +1,154 @@
+/*
+ * vsrk — C ABI of the MI355X (gfx950) kernels behind the cardiac cine-MRI
+ * super-resolution train/eval step.
+ *
+ * Drop-in boundary.  The reference (yangsenwxy/VSR) builds its generators from
+ * stock torch.nn modules and reaches native code only through the DCN
+ * pybind11 module (src/model/nets/edvr_net/dcn/src/deform_conv_cuda.cpp:681-695).
+ * Every entry point below replaces one torch.nn op the reference calls on the
+ * hot path; the replaced call site is cited next to each declaration.
+ *
+ * Conventions
+ *  - Plain C: pointers, sizes, a hipStream_t passed as void*.  No torch types.
+ *  - The caller owns every buffer (device memory), including workspaces sized
+ *    by the *_workspace_size queries.  Nothing here allocates or synchronises,
+ *    so every call is safe inside hipGraph capture.
+ *  - Every call returns 0 (VSRK_OK) or an error code; vsrk_last_error() gives
+ *    the text for the calling thread.
+ *  - Activations are channels-last (N, D, H, W, C) "views" (vsrk_tensor5) with
+ *    element strides; 2-D maps use D = 1.  dtype is VSRK_F32 or VSRK_BF16 and
+ *    applies to activations; weights handed in by the caller are fp32 in the
+ *    torch layout, accumulation is always fp32.
+ */
+#ifndef VSRK_H
+#define VSRK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  VSRK_OK = 0,
+  VSRK_ERR_INVALID = 1,      /* bad argument / unsupported shape */
+  VSRK_ERR_UNSUPPORTED = 2,  /* valid request this build does not implement */
+  VSRK_ERR_LAUNCH = 3        /* HIP launch failure */
+};
+
+enum { VSRK_F32 = 0, VSRK_BF16 = 1 };
+
+enum { VSRK_PRO_NONE = 0, VSRK_PRO_RELU = 1, VSRK_PRO_AFFINE = 2, VSRK_PRO_AFFINE_RELU = 3 };
+enum { VSRK_ACT_NONE = 0, VSRK_ACT_RELU = 1 };
+
+/* Channels-last view.  Element (n,d,h,w,c) lives at
+ *   ptr + n*sn + d*sd + h*sh + w*sw + c                      (shuffle <= 1)
+ * With shuffle = r > 1 the view is the sub-pixel (space-to-depth) image of a
+ * physical tensor P of shape (n, d, h*r, w*r, c/(r*r)) whose strides are
+ * sn..sw:  logical channel c = (i*r + j) * (c/(r*r)) + c' addresses
+ * P[n, d, h*r + i, w*r + j, c'].  Writing a conv output through such a view
+ * is a fused nn.PixelShuffle(r) (edsr_net.py:62, drf_net.py:142); reading
+ * through one is the fused inverse.  The channel order differs from torch's
+ * pixel_shuffle (c'*r*r + i*r + j); vsrk_conv_pack_weight(..., perm_r) and
+ * vsrk_conv_wgrad(..., perm_r) translate. */
+typedef struct vsrk_tensor5 {
+  void* ptr;
+  int32_t n, d, h, w, c;
+  int64_t sn, sd, sh, sw;
+  int32_t shuffle;
+  int32_t dtype;
+} vsrk_tensor5;
+
+/* Stride-1 3-D convolution (2-D when kd = 1 and D = 1), zero padding.
+ * out(n,do,ho,wo,co) = act(out_scale * (bias[co] + sum_{tap,ci} in(n, do+kd-pd,
+ * ho+kh-ph, wo+kw-pw, ci) * W[co,ci,tap])) [* (mask > 0)] [+ residual] [+ out].
+ * The input passes through the prologue first (per-channel scale/shift and/or
+ * ReLU: a fused BatchNorm3d+ReLU, duf_net.py:198-203). */
+typedef struct vsrk_conv_desc {
+  int32_t kd, kh, kw;
+  int32_t pd, ph, pw;
+  int32_t prologue;   /* VSRK_PRO_* applied to every in-bounds input element */
+  int32_t act;        /* VSRK_ACT_* */
+  float out_scale;    /* multiplies (acc + bias) — EDSR res_scale (edsr_net.py:51) */
+  int32_t accumulate; /* 1: out += result (gradient accumulation into concat buffers) */
+  int32_t bias_perm_r; /* >1: bias is in torch pixel-shuffle order (see vsrk_conv_pack_weight perm_r) */
+} vsrk_conv_desc;
+
+/* Repack an fp32 torch conv weight (cout, cin, kd, kh, kw) into the kernel
+ * layout [kd][kh][kw][round_up(cout',32)][round_up(cin',32)] of `dtype`.
+ * mode 0: forward (cout' = cout, cin' = cin).
+ * mode 1: data-gradient (cout' = cin, cin' = cout, taps flipped): the packed
+ *         weight turns vsrk_conv_fwd into dL/dinput of the forward conv with
+ *         padding k-1-p.
+ * perm_r > 1: the torch `cout` index is read in pixel-shuffle order so that a
+ *         conv written through a shuffle-r output view equals torch's
+ *         conv -> PixelShuffle(r).
+ * packed must hold vsrk_conv_packed_elems(...) elements. */
+size_t vsrk_conv_packed_elems(int32_t cout, int32_t cin, int32_t kd, int32_t kh, int32_t kw, int32_t mode);
+int vsrk_conv_pack_weight(int32_t dtype, const float* w, int32_t cout, int32_t cin, int32_t kd,
+                          int32_t kh, int32_t kw, int32_t mode, int32_t perm_r, void* packed,
+                          void* stream);
+
+/* Forward conv, nn.Conv2d / nn.Conv3d forward (edsr_net.py:28-64,
+ * duf_net.py:35-49,116-214, drf_net.py:55-147).  Also the data-gradient of the
+ * same conv when given a mode-1 packed weight and the gradient as `x`.
+ * bias, pro_scale, pro_shift may be NULL; residual, mask may be NULL. */
+int vsrk_conv_fwd(const vsrk_conv_desc* desc, const vsrk_tensor5* x, const void* w_packed,
+                  const float* bias, const float* pro_scale, const float* pro_shift,
+                  const vsrk_tensor5* residual, const vsrk_tensor5* mask,
+                  const vsrk_tensor5* y, void* stream);
+
+/* Weight/bias gradient (autograd of nn.Conv*d.weight/.bias in loss.backward(),
+ * base_trainer.py:128).  dw is fp32 in torch layout (cout, cin, kd, kh, kw);
+ * `perm_r` as in vsrk_conv_pack_weight.  Deterministic: per-workgroup fp32
+ * partial slabs reduced in a fixed order (no float atomics).  dy_scale scales
+ * both gradients; accumulate != 0 adds into dw / dbias.  dbias may be NULL. */
+size_t vsrk_conv_wgrad_workspace_size(const vsrk_conv_desc* desc, const vsrk_tensor5* x,
+                                      const vsrk_tensor5* dy);
+int vsrk_conv_wgrad(const vsrk_conv_desc* desc, const vsrk_tensor5* x, const vsrk_tensor5* dy,
+                    const float* pro_scale, const float* pro_shift, float dy_scale, int32_t perm_r,
+                    float* dw, float* dbias, int32_t accumulate, void* workspace,
+                    size_t workspace_bytes, void* stream);
+
+/* Layout/dtype moves between torch's NC(D)HW fp32 tensors and channels-last
+ * views: src is (n, c, d, h, w) fp32 contiguous; channels beyond c in dst are
+ * zero-filled (input padding for the 1-channel head convs). */
+int vsrk_ncdhw_to_view(const float* src, int32_t n, int32_t c, int32_t d, int32_t h, int32_t w,
+                       const vsrk_tensor5* dst, void* stream);
+int vsrk_view_to_ncdhw(const vsrk_tensor5* src, float* dst, int32_t c, void* stream);
+
+/* Elementwise ReLU backward: dx = dy * (y > 0) (nn.ReLU, edsr_net.py:46). */
+int vsrk_relu_bwd(const vsrk_tensor5* y, const vsrk_tensor5* dy, const vsrk_tensor5* dx, void* stream);
+
+/* Sum of two views into a third (gradient merge at skip connections). */
+int vsrk_add(const vsrk_tensor5* a, const vsrk_tensor5* b, const vsrk_tensor5* out, void* stream);
+
+/* Losses (fp32, mean reduction): kind 0 = L1Loss, 1 = MSELoss, 2 = HuberLoss
+ * (losses.py:5-20, param = delta), 3 = CharbonnierLoss (losses.py:23-34,
+ * param = epsilon).  out/target are `count` contiguous fp32.  loss_fwd writes
+ * the scalar to *loss (device).  loss_bwd writes dL/dout * (*gscale) with
+ * gscale a device scalar (the upstream gradient) to `grad` in dtype. */
+size_t vsrk_loss_workspace_size(int64_t count);
+int vsrk_loss_fwd(int32_t kind, float param, const float* out, const float* target, int64_t count,
+                  float* loss, void* workspace, size_t workspace_bytes, void* stream);
+int vsrk_loss_bwd(int32_t kind, float param, const float* out, const float* target, int64_t count,
+                  const float* gscale, void* grad, int32_t grad_dtype, void* stream);
+
+/* [Denormalize +] PSNR (utils.py:1-20 then metrics.py:20-36): for each of the
+ * `batch` samples of `per_sample` fp32 values, when denormalize != 0
+ * x -> clamp(round(x*std+mean),0,255) (round half to even, as torch.round);
+ * mse over the sample, psnr = 10*log10(max^2/(mse+1e-10)).  Writes per-sample
+ * PSNR to psnr_per_sample[batch] and their mean to *psnr_mean (device). */
+size_t vsrk_psnr_workspace_size(int32_t batch, int64_t per_sample);
+int vsrk_psnr(const float* out, const float* target, int32_t batch, int64_t per_sample, int32_t denormalize,
+              float mean, float std, float max_value, float* psnr_per_sample, float* psnr_mean, void* workspace,
+              size_t workspace_bytes, void* stream);
+
+const char* vsrk_last_error(void);
+const char* vsrk_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VSRK_H */

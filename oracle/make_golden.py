@@ -1,0 +1,182 @@
+"""TEST INFRASTRUCTURE ONLY — pin the CPU restatement to the reference and
+write golden fixtures.
+
+Run in the build container (needs /root/reference):
+    python -m oracle.make_golden
+
+For every case it (1) builds the reference module (imported by path via
+oracle.ref_loader) and the restatement (oracle.cpu_nets) from the same seed,
+(2) asserts identical initial parameters, forward outputs and parameter
+gradients bit for bit on fp32 CPU, and (3) writes tests/golden/<case>.pt
+(inputs, expected output, loss, PSNR, gradient checksums and a few full
+gradient tensors; loadable with torch.load(weights_only=True)).
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+
+import torch
+
+from . import cpu_nets, ref_loader
+
+OUT = Path(__file__).resolve().parent.parent / "tests" / "golden"
+
+CASES = {
+    # name: (ref module, ref class, restatement class, kwargs, input kind, input shape)
+    "edsr_x4_small": ("src.model.nets.edsr_net", "EDSRNet", cpu_nets.EDSRRef,
+                      dict(in_channels=1, out_channels=1, num_resblocks=2, num_features=16, upscale_factor=4),
+                      "sisr", (2, 1, 12, 20)),
+    "edsr_x3_small": ("src.model.nets.edsr_net", "EDSRNet", cpu_nets.EDSRRef,
+                      dict(in_channels=1, out_channels=1, num_resblocks=1, num_features=16, upscale_factor=3),
+                      "sisr", (2, 1, 10, 9)),
+    "edsr_x2_cfg1": ("src.model.nets.edsr_net", "EDSRNet", cpu_nets.EDSRRef,
+                     dict(in_channels=1, out_channels=1, num_resblocks=16, num_features=64, upscale_factor=2),
+                     "sisr", (2, 1, 16, 16)),
+    "edsr_x4_canon": ("src.model.nets.edsr_net", "EDSRNet", cpu_nets.EDSRRef,
+                      dict(in_channels=1, out_channels=1, num_resblocks=16, num_features=64, upscale_factor=4),
+                      "sisr", (2, 1, 12, 16)),
+    "duf_x4_canon": ("src.model.nets.duf_net", "DUFNet", cpu_nets.DUFRef,
+                     dict(in_channels=1, out_channels=1, num_frames=7, size_filter=5, upscale_factor=4,
+                          backbone="_DenseLayer16"),
+                     "misr", (2, 7, 1, 12, 16)),
+    "drf_x4_canon": ("src.model.nets.drf_net", "DRFNet", cpu_nets.DRFRef,
+                     dict(in_channels=1, out_channels=1, num_features=64, num_groups=4, upscale_factor=4),
+                     "vsr", (1, 3, 1, 8, 12)),
+    "drf_sisr_x2_small": ("src.model.nets.drf_sisr_net", "DRFSISRNet", cpu_nets.DRFSISRRef,
+                          dict(in_channels=1, out_channels=1, num_steps=2, num_features=16, num_groups=2,
+                               upscale_factor=2),
+                          "sisr_list", (2, 1, 8, 8)),
+}
+
+SEED = 1234
+# full gradient tensors kept in the fixture (small ones); the rest as checksums
+FULL_GRAD_MAX = 20000
+
+
+def _inputs(kind, shape, r, g):
+    if kind in ("sisr", "sisr_list"):
+        lr = torch.randn(shape, generator=g)
+        hr = torch.randn((shape[0], shape[1], shape[2] * r, shape[3] * r), generator=g)
+        return lr, hr
+    b, t, c, h, w = shape
+    lr = [torch.randn((b, c, h, w), generator=g) for _ in range(t)]
+    if kind == "misr":
+        return lr, torch.randn((b, c, h * r, w * r), generator=g)
+    return lr, [torch.randn((b, c, h * r, w * r), generator=g) for _ in range(t)]
+
+
+def _loss(out, target):
+    # L1 as the reference trainers do: per-frame mean for VSR (acdc_vsr_trainer.py:74-88);
+    # every step against the one target for SISR feedback nets (acdc_sisr_srfb_trainer.py:12-26)
+    if isinstance(out, list) and not isinstance(target, list):
+        return torch.stack([torch.nn.functional.l1_loss(o, target) for o in out]).mean()
+    if isinstance(out, list):
+        return torch.stack([torch.nn.functional.l1_loss(o, t) for o, t in zip(out, target)]).mean()
+    return torch.nn.functional.l1_loss(out, target)
+
+
+def _psnr(out, target, dataset="acdc"):
+    if isinstance(out, list) and not isinstance(target, list):  # last step only (acdc_sisr_srfb_trainer.py:28-38)
+        out = out[-1]
+    if isinstance(out, list):
+        return torch.stack([cpu_nets.psnr(cpu_nets.denormalize(o, dataset), cpu_nets.denormalize(t, dataset))
+                            for o, t in zip(out, target)]).mean()
+    return cpu_nets.psnr(cpu_nets.denormalize(out, dataset), cpu_nets.denormalize(target, dataset))
+
+
+def run_case(name, spec):
+    modname, clsname, mine_cls, kwargs, kind, shape = spec
+    ref_cls = getattr(ref_loader.load(modname), clsname)
+    r = kwargs["upscale_factor"]
+    torch.manual_seed(SEED)
+    ref = ref_cls(**kwargs)
+    torch.manual_seed(SEED)
+    mine = mine_cls(**kwargs)
+    rsd, msd = ref.state_dict(), mine.state_dict()
+    assert list(rsd) == list(msd), f"{name}: state_dict keys differ"
+    for k in rsd:
+        assert torch.equal(rsd[k], msd[k]), f"{name}: init of {k} differs"
+    g = torch.Generator().manual_seed(SEED + 1)
+    lr, hr = _inputs(kind, shape, r, g)
+    outs, grads, losses = [], [], []
+    for net in (ref, mine):
+        net.train()
+        net.zero_grad(set_to_none=True)
+        out = net(lr)
+        loss = _loss(out, hr)
+        loss.backward()
+        outs.append(out)
+        losses.append(loss.detach())
+        grads.append({k: p.grad.detach().clone() for k, p in net.named_parameters()})
+    o_ref, o_mine = outs
+    if isinstance(o_ref, list):
+        for a, b in zip(o_ref, o_mine):
+            assert torch.equal(a, b), f"{name}: outputs differ"
+    else:
+        assert torch.equal(o_ref, o_mine), f"{name}: outputs differ"
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), f"{name}: grad {k} differs"
+    # running stats after one train step (BatchNorm, DUF)
+    buffers = {k: v.clone() for k, v in mine.state_dict().items() if "running" in k}
+    out = o_mine
+    fx = {
+        "name": name, "class": clsname, "kwargs": kwargs, "seed": SEED, "kind": kind,
+        "param_sum": {k: float(v.double().sum()) for k, v in msd.items() if v.is_floating_point()},
+        "lr": lr, "hr": hr,
+        "output": [o.detach() for o in out] if isinstance(out, list) else out.detach(),
+        "loss_l1": float(losses[1]),
+        "psnr_acdc": float(_psnr([o.detach() for o in out] if isinstance(out, list) else out.detach(), hr)),
+        "grad_norm": {k: float(v.double().norm()) for k, v in grads[1].items()},
+        "grad_sum": {k: float(v.double().sum()) for k, v in grads[1].items()},
+        "grad_full": {k: v for k, v in grads[1].items() if v.numel() <= FULL_GRAD_MAX},
+        "running_stats": buffers,
+    }
+    OUT.mkdir(parents=True, exist_ok=True)
+    torch.save(fx, OUT / f"{name}.pt")
+    size = os.path.getsize(OUT / f"{name}.pt")
+    print(f"{name}: restatement == reference (bitwise), loss={fx['loss_l1']:.6f} psnr={fx['psnr_acdc']:.4f} "
+          f"fixture {size / 1024:.0f} KiB")
+
+
+def run_metrics():
+    """Losses (torch.nn + losses.py) and PSNR/SSIM (metrics.py) on fixed data."""
+    losses = ref_loader.load("src.model.losses")
+    metrics = ref_loader.load("src.model.metrics")
+    utils = ref_loader.load("src.utils")
+    g = torch.Generator().manual_seed(7)
+    o = torch.randn((3, 1, 33, 40), generator=g)
+    t = torch.randn((3, 1, 33, 40), generator=g)
+    fx = {"out": o, "target": t, "loss": {}, "grad": {}}
+    for name, fn in (("L1Loss", torch.nn.L1Loss()), ("MSELoss", torch.nn.MSELoss()),
+                     ("HuberLoss", losses.HuberLoss(delta=0.7)), ("CharbonnierLoss", losses.CharbonnierLoss(1e-3))):
+        oo = o.clone().requires_grad_(True)
+        val = fn(oo, t)
+        val.backward()
+        fx["loss"][name] = float(val.detach())
+        fx["grad"][name] = oo.grad.clone()
+    fx["loss_params"] = {"HuberLoss": 0.7, "CharbonnierLoss": 1e-3}
+    for ds in ("acdc", "dsb15"):
+        od, td = utils.denormalize(o, ds), utils.denormalize(t, ds)
+        assert torch.equal(od, cpu_nets.denormalize(o, ds))
+        p_ref = metrics.PSNR()(od, td)
+        p_mine = cpu_nets.psnr(od, td)
+        assert torch.equal(p_ref, p_mine)
+        fx[f"psnr_{ds}"] = float(p_ref)
+        fx[f"psnr_{ds}_per_sample"] = metrics.PSNR(size_average=False)(od, td)
+        fx[f"ssim_{ds}"] = float(metrics.SSIM()(od, td))
+    torch.save(fx, OUT / "metrics.pt")
+    print(f"metrics: psnr_acdc={fx['psnr_acdc']:.4f} ssim_acdc={fx['ssim_acdc']:.4f}")
+
+
+def main():
+    if not ref_loader.available():
+        raise SystemExit("reference not available (build container only)")
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    for name, spec in CASES.items():
+        run_case(name, spec)
+    run_metrics()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,183 @@
+"""Parity of the implicit-GEMM conv kernels (forward, data-gradient, weight
+gradient) against torch fp64 on the CPU (the oracle for a floating-point
+kernel), across the shapes the generators use and the fused prologue /
+epilogue / sub-pixel addressing modes.
+
+Tolerances: fp32 kernels: max |d| <= 2e-5 * (1 + max|ref|) (exact-fp32 MFMA,
+different summation order).  bf16 kernels: inputs and weights are rounded to
+bf16 before the fp64 reference, so only accumulation order and the final bf16
+store differ: max |d| <= 1.5e-2 * max|ref|.
+"""
+import pytest
+import torch
+import torch.nn.functional as Fn
+
+from vsr_amd import functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _tol(dtype, ref):
+    scale = ref.abs().max().item()
+    return (2e-5 * (1 + scale)) if dtype == torch.float32 else 1.5e-2 * max(scale, 1e-3)
+
+
+def _q(t, dtype):
+    """round to the compute dtype (what the kernel sees), back to fp64."""
+    return t.to(dtype).double()
+
+
+def _ref_conv(x_cl, w, b, pad):
+    # x_cl (N,D,H,W,C) -> NCDHW fp64 conv3d -> (N,D,H,W,Co)
+    x = x_cl.permute(0, 4, 1, 2, 3)
+    y = Fn.conv3d(x, w, b, padding=pad)
+    return y.permute(0, 2, 3, 4, 1)
+
+
+CASES = [
+    # (N, D, H, W, Cin, Cout, k, pad)
+    (2, 1, 13, 37, 16, 32, (1, 3, 3), (0, 1, 1)),
+    (1, 1, 9, 70, 64, 64, (1, 3, 3), (0, 1, 1)),
+    (2, 5, 9, 35, 24, 40, (3, 3, 3), (1, 1, 1)),
+    (1, 7, 6, 20, 48, 32, (3, 3, 3), (0, 1, 1)),
+    (2, 3, 5, 33, 48, 130, (1, 1, 1), (0, 0, 0)),
+    (2, 1, 11, 12, 1, 64, (1, 3, 3), (0, 1, 1)),
+    (2, 1, 17, 19, 64, 1, (1, 3, 3), (0, 1, 1)),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES)
+def test_conv_forward(case, dtype):
+    n, d, h, w, ci, co, k, pad = case
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn((n, d, h, w, ci), generator=g)
+    wt = torch.randn((co, ci, *k), generator=g) / (ci * k[0] * k[1] * k[2]) ** 0.5
+    b = torch.randn(co, generator=g)
+    ref = _ref_conv(_q(x, dtype), _q(wt, dtype), b.double(), pad)
+    do = d + 2 * pad[0] - k[0] + 1
+    xd = x.to(DEV, dtype)
+    y = torch.empty((n, do, h, w, co), dtype=dtype, device=DEV)
+    F.conv(xd, F.pack_weight(wt.to(DEV), 0, dtype), y, k, pad, bias=b.to(DEV))
+    err = (y.double().cpu() - ref).abs().max().item()
+    assert err <= _tol(dtype, ref), err
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_fused_prologue_epilogue(dtype):
+    """BN-affine+ReLU prologue, ReLU act, out_scale, mask, residual, accumulate,
+    on channel-slice views of larger buffers (the DUF concat layout)."""
+    g = torch.Generator().manual_seed(1)
+    n, d, h, w, ci, co = 2, 3, 10, 40, 32, 32
+    big = torch.randn((n, d, h, w, ci + 16), generator=g)
+    x = big[..., 8:8 + ci]
+    wt = torch.randn((co, ci, 3, 3, 3), generator=g) / 12
+    b = torch.randn(co, generator=g)
+    sc = torch.rand(ci, generator=g) + 0.5
+    sh = torch.randn(ci, generator=g)
+    mask = torch.randn((n, d, h, w, co), generator=g)
+    res = torch.randn((n, d, h, w, co), generator=g)
+    y0 = torch.randn((n, d, h, w, co), generator=g)
+    xin = torch.relu(_q(x, dtype) * sc.double() + sh.double())
+    xin = xin.to(dtype).double() if dtype != torch.float32 else xin
+    ref = torch.relu(_ref_conv(xin, _q(wt, dtype), b.double(), (1, 1, 1)) * 0.5)
+    ref = torch.where(_q(mask, dtype) > 0, ref, torch.zeros_like(ref)) + _q(res, dtype) + _q(y0, dtype)
+    bigd = big.to(DEV, dtype)
+    yd = y0.to(DEV, dtype)
+    F.conv(bigd[..., 8:8 + ci], F.pack_weight(wt.to(DEV), 0, dtype), yd, (3, 3, 3), (1, 1, 1), bias=b.to(DEV),
+           prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV), act=F.ACT_RELU, out_scale=0.5,
+           mask=mask.to(DEV, dtype), residual=res.to(DEV, dtype), accumulate=True)
+    err = (yd.double().cpu() - ref).abs().max().item()
+    assert err <= _tol(dtype, ref) * 2, err
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("r", [2, 3])
+def test_conv_pixel_shuffle_output(dtype, r):
+    """conv written through a sub-pixel view == torch conv2d -> pixel_shuffle."""
+    g = torch.Generator().manual_seed(2)
+    n, h, w, ci, f = 2, 7, 33, 16, 16
+    co = f * r * r
+    x = torch.randn((n, 1, h, w, ci), generator=g)
+    wt = torch.randn((co, ci, 3, 3), generator=g) / 12
+    b = torch.randn(co, generator=g)
+    ref = Fn.pixel_shuffle(Fn.conv2d(_q(x, dtype)[:, 0].permute(0, 3, 1, 2), _q(wt, dtype), b.double(), padding=1), r)
+    ref = ref.permute(0, 2, 3, 1)  # (n, rh, rw, f)
+    y = torch.empty((n, 1, h * r, w * r, f), dtype=dtype, device=DEV)
+    F.conv(x.to(DEV, dtype), F.pack_weight(wt.to(DEV), 0, dtype, perm_r=r), y, (1, 3, 3), (0, 1, 1),
+           bias=b.to(DEV), y_shuffle=r)
+    err = (y[:, 0].double().cpu() - ref).abs().max().item()
+    assert err <= _tol(dtype, ref), err
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES)
+def test_conv_backward(case, dtype):
+    """data-gradient (mode-1 packed weight through the forward kernel) and the
+    deterministic weight/bias gradient against torch autograd in fp64."""
+    n, d, h, w, ci, co, k, pad = case
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn((n, d, h, w, ci), generator=g)
+    wt = torch.randn((co, ci, *k), generator=g) / (ci * k[0] * k[1] * k[2]) ** 0.5
+    b = torch.randn(co, generator=g)
+    do = d + 2 * pad[0] - k[0] + 1
+    gy = torch.randn((n, do, h, w, co), generator=g)
+    xr = _q(x, dtype).requires_grad_(True)
+    wr = _q(wt, dtype).requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    yr = _ref_conv(xr, wr, br, pad)
+    yr.backward(_q(gy, dtype))
+    # dgrad
+    dpad = tuple(kk - 1 - p for kk, p in zip(k, pad))
+    dx = torch.empty((n, d, h, w, ci), dtype=dtype, device=DEV)
+    F.conv(gy.to(DEV, dtype), F.pack_weight(wt.to(DEV), 1, dtype), dx, k, dpad)
+    err = (dx.double().cpu() - xr.grad).abs().max().item()
+    assert err <= _tol(dtype, xr.grad), ("dgrad", err)
+    # wgrad
+    dw = torch.empty((co, ci, *k), dtype=torch.float32, device=DEV)
+    db = torch.empty(co, dtype=torch.float32, device=DEV)
+    F.conv_wgrad(x.to(DEV, dtype), gy.to(DEV, dtype), k, pad, dw, db)
+    ew = (dw.double().cpu() - wr.grad).abs().max().item()
+    eb = (db.double().cpu() - br.grad).abs().max().item()
+    tw = (2e-5 if dtype == torch.float32 else 1e-2) * (1 + wr.grad.abs().max().item())
+    tb = (2e-5 if dtype == torch.float32 else 1e-2) * (1 + br.grad.abs().max().item())
+    assert ew <= tw, ("wgrad", ew, tw)
+    assert eb <= tb, ("bgrad", eb, tb)
+
+
+def test_wgrad_deterministic():
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn((2, 4, 16, 40, 32), generator=g).to(DEV, torch.bfloat16)
+    gy = torch.randn((2, 4, 16, 40, 32), generator=g).to(DEV, torch.bfloat16)
+    outs = []
+    for _ in range(2):
+        dw = torch.empty((32, 32, 3, 3, 3), device=DEV)
+        F.conv_wgrad(x, gy, (3, 3, 3), (1, 1, 1), dw)
+        outs.append(dw)
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_wgrad_prologue_and_shuffle(dtype):
+    """weight gradient with BN-affine+ReLU prologue on x and a sub-pixel dy view."""
+    g = torch.Generator().manual_seed(5)
+    r, n, h, w, ci, f = 2, 2, 6, 20, 16, 16
+    co = f * r * r
+    x = torch.randn((n, 1, h, w, ci), generator=g)
+    sc = torch.rand(ci, generator=g) + 0.5
+    sh = torch.randn(ci, generator=g)
+    wt = torch.randn((co, ci, 3, 3), generator=g) / 12
+    gy = torch.randn((n, f, h * r, w * r), generator=g)  # grad of the shuffled output (NCHW)
+    xin = torch.relu(_q(x, dtype) * sc.double() + sh.double())
+    xin = xin.to(dtype).double() if dtype != torch.float32 else xin
+    wr = _q(wt, dtype).requires_grad_(True)
+    y = Fn.pixel_shuffle(Fn.conv2d(xin[:, 0].permute(0, 3, 1, 2), wr, padding=1), r)
+    y.backward(_q(gy, dtype))
+    dw = torch.empty((co, ci, 3, 3), device=DEV)
+    gy_cl = gy.permute(0, 2, 3, 1).unsqueeze(1).contiguous().to(DEV, dtype)  # (n,1,rh,rw,f)
+    F.conv_wgrad(x.to(DEV, dtype), gy_cl, (1, 3, 3), (0, 1, 1), dw.view(co, ci, 1, 3, 3),
+                 prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV), perm_r=r, dy_shuffle=r)
+    err = (dw.double().cpu() - wr.grad).abs().max().item()
+    tol = (2e-5 if dtype == torch.float32 else 1e-2) * (1 + wr.grad.abs().max().item())
+    assert err <= tol, err

@@ -1,0 +1,69 @@
+"""Builds the HIP kernels (gfx950) into the in-tree C-ABI library
+``vsr_amd/_lib/libvsrk.so`` with plain ``hipcc`` (no torch headers involved:
+the boundary is the C ABI declared in ``include/vsrk.h``)."""
+from __future__ import annotations
+
+import hashlib
+import os
+import subprocess
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+CSRC = ROOT / "csrc"
+LIBDIR = ROOT / "_lib"
+LIB = LIBDIR / "libvsrk.so"
+INCLUDE = ROOT.parent / "include"
+ARCH = os.environ.get("VSRK_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+
+
+def sources() -> list[Path]:
+    return sorted(CSRC.glob("*.hip"))
+
+
+def _digest() -> str:
+    h = hashlib.sha256()
+    for p in sources() + sorted(CSRC.glob("*.h")) + [INCLUDE / "vsrk.h"]:
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile every ``csrc/*.hip`` and link ``libvsrk.so``; skipped when the
+    sources are unchanged since the last build (digest stamp)."""
+    LIBDIR.mkdir(exist_ok=True)
+    stamp = LIBDIR / "libvsrk.stamp"
+    digest = _digest()
+    if not force and LIB.exists() and stamp.exists() and stamp.read_text() == digest:
+        return LIB
+    objdir = LIBDIR / "obj"
+    objdir.mkdir(exist_ok=True)
+
+    def compile_one(src: Path) -> Path:
+        obj = objdir / (src.stem + ".o")
+        cmd = [HIPCC, *FLAGS, "-I", str(INCLUDE), "-c", str(src), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-6000:]}")
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(8, len(sources()))) as ex:
+        objs = list(ex.map(compile_one, sources()))
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", *[str(o) for o in objs], "-o", str(tmp)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+    os.replace(tmp, LIB)
+    stamp.write_text(digest)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

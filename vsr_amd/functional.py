@@ -1,0 +1,193 @@
+"""Thin Python layer over the vsrk C ABI (include/vsrk.h).
+
+Activations are channels-last tensors shaped (N, D, H, W, C) — 2-D feature
+maps use D = 1 — in the compute dtype (bfloat16 or float32).  Every function
+launches native HIP kernels on torch's current stream; none of them has a
+CPU or PyTorch fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _native as N
+from ._native import ACT_NONE, ACT_RELU, PRO_AFFINE, PRO_AFFINE_RELU, PRO_NONE, PRO_RELU  # noqa: F401
+
+__all__ = [
+    "pack_weight", "conv", "conv_wgrad", "to_view", "from_view", "relu_bwd", "add",
+    "loss_fwd", "loss_bwd", "psnr", "workspace", "LOSS_KINDS",
+]
+
+LOSS_KINDS = {"L1Loss": 0, "MSELoss": 1, "HuberLoss": 2, "CharbonnierLoss": 3}
+
+_ws: dict[int, torch.Tensor] = {}
+
+
+def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
+    """A per-device scratch buffer (grown on demand, stream-ordered reuse)."""
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    buf = _ws.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _ws[key] = buf
+    return buf
+
+
+def _lib():
+    return N.load()
+
+
+def _kdims(w: torch.Tensor) -> tuple[int, int, int]:
+    if w.dim() == 5:
+        return tuple(w.shape[2:])
+    if w.dim() == 4:
+        return (1, w.shape[2], w.shape[3])
+    raise ValueError(f"conv weight must be 4-D or 5-D, got {tuple(w.shape)}")
+
+
+def pack_weight(w: torch.Tensor, mode: int, dtype: torch.dtype, perm_r: int = 1) -> torch.Tensor:
+    """Repack an fp32 torch conv weight (cout, cin, [kd,] kh, kw) for the kernel.
+    mode 0 = forward, mode 1 = data-gradient (transposed, flipped taps)."""
+    lib = _lib()
+    cout, cin = w.shape[:2]
+    kd, kh, kw = _kdims(w)
+    n = lib.vsrk_conv_packed_elems(cout, cin, kd, kh, kw, mode)
+    out = torch.empty(n, dtype=dtype, device=w.device)
+    wc = w.detach()
+    if wc.dtype != torch.float32 or not wc.is_contiguous():
+        wc = wc.float().contiguous()
+    N.check(lib.vsrk_conv_pack_weight(N.dtype_code(dtype), wc.data_ptr(), cout, cin, kd, kh, kw, mode, perm_r,
+                                      out.data_ptr(), N.stream_ptr(w.device)), "conv_pack_weight")
+    return out
+
+
+def _desc(k, pad, prologue=PRO_NONE, act=ACT_NONE, out_scale=1.0, accumulate=False, bias_r=1) -> N.ConvDesc:
+    kd, kh, kw = k
+    pd, ph, pw = pad
+    return N.ConvDesc(kd, kh, kw, pd, ph, pw, prologue, act, float(out_scale), 1 if accumulate else 0, bias_r)
+
+
+def conv(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, *, bias: torch.Tensor | None = None,
+         prologue: int = PRO_NONE, pro_scale: torch.Tensor | None = None, pro_shift: torch.Tensor | None = None,
+         act: int = ACT_NONE, out_scale: float = 1.0, accumulate: bool = False,
+         residual: torch.Tensor | None = None, mask: torch.Tensor | None = None,
+         x_shuffle: int = 1, y_shuffle: int = 1) -> torch.Tensor:
+    """y[...] = epilogue(conv(prologue(x), W) + bias); writes into the given y view.
+
+    residual/mask are views with y's logical shape (and y_shuffle addressing)."""
+    lib = _lib()
+    d = _desc(k, pad, prologue, act, out_scale, accumulate, y_shuffle if bias is not None else 1)
+    xv = N.t5(x, x_shuffle)
+    yv = N.t5(y, y_shuffle)
+    rv = N.t5(residual, y_shuffle) if residual is not None else None
+    mv = N.t5(mask, y_shuffle) if mask is not None else None
+    rc = lib.vsrk_conv_fwd(C.byref(d), C.byref(xv), wp.data_ptr(), N.ptr(bias), N.ptr(pro_scale),
+                           N.ptr(pro_shift), C.byref(rv) if rv is not None else None,
+                           C.byref(mv) if mv is not None else None, C.byref(yv), N.stream_ptr(x.device))
+    N.check(rc, "conv_fwd")
+    return y
+
+
+def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, k, pad, dw: torch.Tensor, dbias: torch.Tensor | None = None, *,
+               prologue: int = PRO_NONE, pro_scale: torch.Tensor | None = None,
+               pro_shift: torch.Tensor | None = None, dy_scale: float = 1.0, perm_r: int = 1,
+               accumulate: bool = False, x_shuffle: int = 1, dy_shuffle: int = 1) -> None:
+    """dw (fp32, torch layout) [+]= dy_scale * dL/dW; dbias likewise."""
+    lib = _lib()
+    d = _desc(k, pad, prologue)
+    xv = N.t5(x, x_shuffle)
+    gv = N.t5(dy, dy_shuffle)
+    assert dw.dtype == torch.float32 and dw.is_contiguous()
+    nbytes = lib.vsrk_conv_wgrad_workspace_size(C.byref(d), C.byref(xv), C.byref(gv))
+    ws = workspace(nbytes, x.device)
+    rc = lib.vsrk_conv_wgrad(C.byref(d), C.byref(xv), C.byref(gv), N.ptr(pro_scale), N.ptr(pro_shift),
+                             float(dy_scale), perm_r, dw.data_ptr(), N.ptr(dbias), 1 if accumulate else 0,
+                             ws.data_ptr(), ws.numel(), N.stream_ptr(x.device))
+    N.check(rc, "conv_wgrad")
+
+
+def to_view(src: torch.Tensor, dtype: torch.dtype, cpad: int | None = None) -> torch.Tensor:
+    """(N, C, [D,] H, W) fp32 -> channels-last (N, D, H, W, cpad) in dtype (zero padded)."""
+    lib = _lib()
+    if src.dim() == 4:
+        n, c, h, w = src.shape
+        d = 1
+    else:
+        n, c, d, h, w = src.shape
+    cp = cpad or c
+    out = torch.empty((n, d, h, w, cp), dtype=dtype, device=src.device)
+    s = src if (src.dtype == torch.float32 and src.is_contiguous()) else src.float().contiguous()
+    v = N.t5(out)
+    N.check(lib.vsrk_ncdhw_to_view(s.data_ptr(), n, c, d, h, w, C.byref(v), N.stream_ptr(src.device)),
+            "ncdhw_to_view")
+    return out
+
+
+def from_view(v: torch.Tensor, c: int | None = None, two_d: bool = True) -> torch.Tensor:
+    """channels-last (N, D, H, W, C) -> fp32 (N, C, H, W) (D must be 1 when two_d) or (N, C, D, H, W)."""
+    lib = _lib()
+    n, d, h, w, cc = v.shape
+    c = c or cc
+    shape = (n, c, h, w) if (two_d and d == 1) else (n, c, d, h, w)
+    out = torch.empty(shape, dtype=torch.float32, device=v.device)
+    tv = N.t5(v)
+    N.check(lib.vsrk_view_to_ncdhw(C.byref(tv), out.data_ptr(), c, N.stream_ptr(v.device)), "view_to_ncdhw")
+    return out
+
+
+def relu_bwd(y: torch.Tensor, dy: torch.Tensor, dx: torch.Tensor) -> torch.Tensor:
+    lib = _lib()
+    a, b, c = N.t5(y), N.t5(dy), N.t5(dx)
+    N.check(lib.vsrk_relu_bwd(C.byref(a), C.byref(b), C.byref(c), N.stream_ptr(y.device)), "relu_bwd")
+    return dx
+
+
+def add(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    lib = _lib()
+    x, y, z = N.t5(a), N.t5(b), N.t5(out)
+    N.check(lib.vsrk_add(C.byref(x), C.byref(y), C.byref(z), N.stream_ptr(a.device)), "add")
+    return out
+
+
+def loss_fwd(kind: int, param: float, out: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """Mean-reduced loss of two fp32 tensors -> device scalar."""
+    lib = _lib()
+    assert out.dtype == torch.float32 and target.dtype == torch.float32
+    o, t = out.contiguous(), target.contiguous()
+    res = torch.empty((), dtype=torch.float32, device=out.device)
+    nb = lib.vsrk_loss_workspace_size(o.numel())
+    ws = torch.empty(nb, dtype=torch.uint8, device=out.device)
+    N.check(lib.vsrk_loss_fwd(kind, float(param), o.data_ptr(), t.data_ptr(), o.numel(), res.data_ptr(),
+                              ws.data_ptr(), nb, N.stream_ptr(out.device)), "loss_fwd")
+    return res
+
+
+def loss_bwd(kind: int, param: float, out: torch.Tensor, target: torch.Tensor, gscale: torch.Tensor | None,
+             dtype: torch.dtype = torch.float32) -> torch.Tensor:
+    lib = _lib()
+    o, t = out.contiguous(), target.contiguous()
+    g = torch.empty(o.shape, dtype=dtype, device=out.device)
+    gs = gscale.float().contiguous() if gscale is not None else None
+    N.check(lib.vsrk_loss_bwd(kind, float(param), o.data_ptr(), t.data_ptr(), o.numel(), N.ptr(gs), g.data_ptr(),
+                              N.dtype_code(dtype), N.stream_ptr(out.device)), "loss_bwd")
+    return g
+
+
+def psnr(out: torch.Tensor, target: torch.Tensor, mean: float = 0.0, std: float = 1.0, max_value: float = 255.0,
+         denormalize: bool = True):
+    """[Denormalize (x*std+mean, round, clamp [0,255]) both,] per-sample PSNR;
+    returns (batch mean, per-sample) as device tensors."""
+    lib = _lib()
+    o = out.float().contiguous()
+    t = target.float().contiguous()
+    b = o.shape[0]
+    per = o.numel() // b
+    ps = torch.empty(b, dtype=torch.float32, device=o.device)
+    m = torch.empty((), dtype=torch.float32, device=o.device)
+    nb = lib.vsrk_psnr_workspace_size(b, per)
+    ws = torch.empty(nb, dtype=torch.uint8, device=o.device)
+    N.check(lib.vsrk_psnr(o.data_ptr(), t.data_ptr(), b, per, 1 if denormalize else 0, float(mean), float(std),
+                          float(max_value),
+                          ps.data_ptr(), m.data_ptr(), ws.data_ptr(), nb, N.stream_ptr(o.device)), "psnr")
+    return m, ps
