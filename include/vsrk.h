@@ -76,7 +76,7 @@ typedef struct vsrk_conv_desc {
 } vsrk_conv_desc;
 
 /* Repack an fp32 torch conv weight (cout, cin, kd, kh, kw) into the kernel
- * layout [kd][kh][kw][round_up(cout',32)][round_up(cin',32)] of `dtype`.
+ * layout [kd][kh][kw][round_up(cout',128)][round_up(cin',32)] of `dtype`.
  * mode 0: forward (cout' = cout, cin' = cin).
  * mode 1: data-gradient (cout' = cin, cin' = cout, taps flipped): the packed
  *         weight turns vsrk_conv_fwd into dL/dinput of the forward conv with

@@ -1,0 +1,182 @@
+// Shared pieces of the implicit-GEMM convolution kernels (conv_fwd.hip,
+// conv_wgrad.hip).  See conv_fwd.hip for the design notes.
+#pragma once
+#include "vsrk_common.h"
+#include "vsrk_internal.h"
+
+namespace vsrk_conv {
+
+
+constexpr int NTHR = 512;  // 8 waves per workgroup
+constexpr int TW = 32;     // tile columns = one MFMA column block
+constexpr int GTH = 8;     // weight-gradient tile rows: 8 x 32 = 256 voxels
+constexpr int ROWB = 80;   // forward LDS bytes per staged input row (64 data + 16 pad)
+constexpr int GTHR = 256;  // weight-gradient workgroup: 4 waves, one per SIMD (512 VGPRs each)
+constexpr int MAXK = 3;    // kh, kw <= 3
+
+// XCD-aware block order: under round-robin dispatch blocks b and b+8 share an
+// XCD; give each XCD a contiguous range of logical tiles so neighbouring
+// tiles' halo rows and the shared weight slices are re-read from one L2.
+// Bijective for any grid size (speed only, never correctness).
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int xcd = bid & 7, q = nblk >> 3, rr = nblk & 7;
+  const int base = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
+  return base + (bid >> 3);
+}
+
+struct ConvArgs {
+  View x, y, res, msk;
+  const char* w;
+  const float* bias;
+  const float* pro_scale;
+  const float* pro_shift;
+  int cin, cout, cin_pad, cout_pad;
+  int kd, kh, kw, pd, ph, pw;
+  int prologue, act, accumulate, has_res, has_mask, xvec, bias_r;
+  float out_scale;
+  int tiles_h, tiles_w, ntn, nblk;
+  int ntiles;  // output tiles (incl. N tiles) walked by the persistent grid
+};
+
+// Zero the channels of a chunk at or beyond `nvalid` (the partial last chunk
+// of a view whose storage is padded: padding may hold anything).
+template <typename T>
+__device__ __forceinline__ uint4 mask_tail(uint4 v, int nvalid) {
+  constexpr int E = Chunk<T>::E;
+  if (nvalid >= E) return v;
+  float f[E];
+  Chunk<T>::unpack(v, f);
+#pragma unroll
+  for (int e = 0; e < E; ++e) f[e] = e < nvalid ? f[e] : 0.f;
+  return Chunk<T>::pack(f);
+}
+
+// Raw 16-byte chunk of channels [c, c+E) at logical voxel (n,d,h,w): one vector
+// load when the view allows it, else element loads (zero past cin).
+template <typename T>
+__device__ __forceinline__ uint4 load_raw(const View& v, int n, int d, int h, int w, int c, int cin, bool vec) {
+  constexpr int E = Chunk<T>::E;
+  const T* p = reinterpret_cast<const T*>(v.ptr) + view_off(v, n, d, h, w, c);
+  if (vec && c + E <= cin) return *reinterpret_cast<const uint4*>(p);
+  float f[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) f[e] = (c + e < cin) ? to_f32<T>(p[e]) : 0.f;
+  return Chunk<T>::pack(f);
+}
+
+// Per-channel affine + optional ReLU (a fused BatchNorm+ReLU) with scale/shift
+// staged in LDS: real channels carry (scale, shift) — (1, 0) for a ReLU-only
+// prologue — padding channels carry (0, 0), so the transform is branchless and
+// padding stays zero.
+template <typename T>
+__device__ __forceinline__ uint4 prologue_lds(uint4 v, int c, bool relu, const float* lsc, const float* lsh) {
+  constexpr int E = Chunk<T>::E;
+  float f[E];
+  Chunk<T>::unpack(v, f);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    float t = fmaf(f[e], lsc[c + e], lsh[c + e]);
+    f[e] = relu ? fmaxf(t, 0.f) : t;
+  }
+  return Chunk<T>::pack(f);
+}
+
+// Stage the prologue's per-channel (scale, shift) into LDS, zero-padded to cpad.
+__device__ __forceinline__ void stage_prologue(float* lsc, float* lsh, int mode, const float* sc, const float* sh,
+                                               int cin, int cpad, int tid, int nthr) {
+  for (int i = tid; i < cpad; i += nthr) {
+    const bool ok = i < cin;
+    const bool aff = (mode & VSRK_PRO_AFFINE) != 0;
+    lsc[i] = ok ? (aff ? sc[i] : 1.f) : 0.f;
+    lsh[i] = ok ? (aff ? sh[i] : 0.f) : 0.f;
+  }
+}
+
+// acc += W(32 rows of co, 16-byte k slice) x X(16-byte k slice, 32 voxels)
+template <typename T>
+__device__ __forceinline__ void mma(f32x16& acc, uint4 a, uint4 b);
+template <>
+__device__ __forceinline__ void mma<bf16>(f32x16& acc, uint4 a, uint4 b) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ void mma<float>(f32x16& acc, uint4 a, uint4 b) {
+  // lane half hf supplies k = 4*hf + j for MFMA j on both operands, so the
+  // four k=2 products cover the 8 channels of the slice exactly once.
+  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__builtin_bit_cast(float, a.x), __builtin_bit_cast(float, b.x), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__builtin_bit_cast(float, a.y), __builtin_bit_cast(float, b.y), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__builtin_bit_cast(float, a.z), __builtin_bit_cast(float, b.z), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__builtin_bit_cast(float, a.w), __builtin_bit_cast(float, b.w), acc, 0, 0, 0);
+}
+
+template <typename YT>
+__device__ __forceinline__ void load4(const char* base, int64_t off, bool vec, int valid, float* v) {
+  const YT* p = reinterpret_cast<const YT*>(base) + off;
+  if (vec) {
+    if constexpr (sizeof(YT) == 4) {
+      float4 t = *reinterpret_cast<const float4*>(p);
+      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else {
+      uint2 t = *reinterpret_cast<const uint2*>(p);
+      const bf16* b = reinterpret_cast<const bf16*>(&t);
+      for (int e = 0; e < 4; ++e) v[e] = (float)b[e];
+    }
+  } else {
+    for (int e = 0; e < 4; ++e) v[e] = e < valid ? to_f32<YT>(p[e]) : 0.f;
+  }
+}
+
+struct WgradArgs {
+  View x, dy;
+  const float* pro_scale;
+  const float* pro_shift;
+  float* ws;
+  int cin, cout;
+  int kd, kh, kw, pd, ph, pw;
+  int prologue, xvec, dyvec;
+  int tiles_h, tiles_w, ntiles, tiles_per_split, nsplit, ncombos, nblk;
+  int n_ci_chunks, n_co_tiles, kd_bias, slab, want_bias, cin_pad;
+};
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+__device__ __forceinline__ v4i16 ds_read_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(p));
+}
+
+}  // namespace vsrk_conv
+
+
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+// Can the kernels read this view in 16-byte chunks?  (aligned base, strides
+// and channel count multiples of one chunk; sub-pixel blocks chunk-aligned)
+static inline bool chunk_ok(const vsrk_tensor5* t, int esize) {
+  // Whole 16-byte chunks may be read at every chunk-aligned channel: aligned
+  // base and strides.  c need not be a multiple of a chunk (channels past c
+  // are masked), but a sub-pixel block must be.
+  const int epc = 16 / esize;
+  const int r = t->shuffle > 1 ? t->shuffle : 1;
+  const bool block_ok = r == 1 || (t->c / (r * r)) % epc == 0;
+  const bool stride_ok = t->sw >= epc || (t->w == 1);
+  return ((uintptr_t)t->ptr) % 16 == 0 && t->sn % epc == 0 && t->sd % epc == 0 && t->sh % epc == 0 &&
+         t->sw % epc == 0 && block_ok && stride_ok;
+}
+
+static inline bool view_ok(const vsrk_tensor5* t, const char* what) {
+  if (!t || !t->ptr) {
+    vsrk_set_error("%s: null view", what);
+    return false;
+  }
+  const int r = t->shuffle > 1 ? t->shuffle : 1;
+  if (t->c % (r * r) != 0 || (r > 1 && (t->c / (r * r)) % 8 != 0)) {
+    vsrk_set_error("%s: sub-pixel view needs channels divisible by 8*shuffle^2 (c=%d, r=%d)", what, t->c, r);
+    return false;
+  }
+  return true;
+}
+

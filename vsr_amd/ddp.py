@@ -1,0 +1,89 @@
+"""Data-parallel gradient synchronisation over RCCL (torch.distributed 'nccl').
+
+The reference is single-device (main.py:38); the build shards minibatches
+across the GPUs of one node (one process per GPU).  GradSync owns flat fp32
+communication buckets: every parameter's .grad is a view into one, the
+hand-written backward passes write gradients straight into those views, and a
+bucket's all-reduce is launched (async, on RCCL's stream) the moment its last
+gradient is written — so communication overlaps the rest of backward instead
+of running after it.  Buckets follow the backward order (reverse registration)
+and are ~4 MiB: the models have 6-10 MB of fp32 gradients, i.e. 2-3 buckets,
+each a single ring all-reduce over xGMI.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class GradSync:
+    def __init__(self, net, world: int, bucket_bytes: int = 4 << 20):
+        self.world = world
+        self.net = net
+        params = [p for p in net.parameters() if p.requires_grad]
+        order = list(reversed(params))
+        self.buckets: list[list[torch.Tensor]] = [[]]
+        size = 0
+        for p in order:
+            if size >= bucket_bytes:
+                self.buckets.append([])
+                size = 0
+            self.buckets[-1].append(p)
+            size += p.numel() * 4
+        dev = params[0].device
+        self.flat: list[torch.Tensor] = []
+        self._view: dict[int, torch.Tensor] = {}
+        self._bucket_of: dict[int, int] = {}
+        for b, ps in enumerate(self.buckets):
+            buf = torch.zeros(sum(p.numel() for p in ps), dtype=torch.float32, device=dev)
+            self.flat.append(buf)
+            off = 0
+            for p in ps:
+                v = buf[off:off + p.numel()].view_as(p)
+                self._view[id(p)] = v
+                self._bucket_of[id(p)] = b
+                off += p.numel()
+        self._params = params
+        self._reset()
+        net._grad_sink = self
+        self._avg = hasattr(dist.ReduceOp, "AVG")
+        self._attach()
+
+    def _reset(self):
+        self._remaining = [len(ps) for ps in self.buckets]
+        self._handles: list = [None] * len(self.buckets)
+
+    def _attach(self):
+        for p in self._params:
+            p.grad = self._view[id(p)]
+
+    def view(self, p: torch.Tensor) -> torch.Tensor:
+        return self._view[id(p)]
+
+    def _launch(self, b: int):
+        op = dist.ReduceOp.AVG if self._avg else dist.ReduceOp.SUM
+        self._handles[b] = dist.all_reduce(self.flat[b], op=op, async_op=True)
+
+    def ready(self, p: torch.Tensor) -> None:
+        b = self._bucket_of[id(p)]
+        self._remaining[b] -= 1
+        if self._remaining[b] == 0:
+            self._launch(b)
+
+    def finish(self) -> None:
+        """Wait for every bucket (launching any not yet complete), average, and
+        re-attach .grad views (zero_grad(set_to_none=True) may have dropped them)."""
+        for b, h in enumerate(self._handles):
+            if h is None:
+                self._launch(b)
+        for b, h in enumerate(self._handles):
+            self._handles[b].wait()
+            if not self._avg:
+                self.flat[b].mul_(1.0 / self.world)
+        self._reset()
+        self._attach()
+
+    def broadcast_params(self, src: int = 0) -> None:
+        """Start from identical weights on every rank."""
+        for p in self._params:
+            dist.broadcast(p.data, src)

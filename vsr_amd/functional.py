@@ -24,6 +24,36 @@ LOSS_KINDS = {"L1Loss": 0, "MSELoss": 1, "HuberLoss": 2, "CharbonnierLoss": 3}
 _ws: dict[int, torch.Tensor] = {}
 
 
+class KernelTimer:
+    """Brackets selected native launches with HIP events on the launch stream
+    (torch's current stream, where every vsrk kernel runs).  `match(kind, x, y)`
+    selects launches; bench.py uses it for the roofline of the dominant kernel."""
+
+    def __init__(self, match):
+        self.match = match
+        self.events: list[tuple[torch.cuda.Event, torch.cuda.Event]] = []
+        self.enabled = True
+
+    def wrap(self, kind, x, y, launch):
+        if not (self.enabled and self.match(kind, x, y)):
+            return launch()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        out = launch()
+        e.record()
+        self.events.append((s, e))
+        return out
+
+    def mean_ms(self) -> float:
+        torch.cuda.synchronize()
+        if not self.events:
+            return float("nan")
+        return sum(s.elapsed_time(e) for s, e in self.events) / len(self.events)
+
+
+timer: KernelTimer | None = None
+
+
 def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
     """A per-device scratch buffer (grown on demand, stream-ordered reuse)."""
     key = device.index if device.index is not None else torch.cuda.current_device()
@@ -82,9 +112,12 @@ def conv(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, *, bias: to
     yv = N.t5(y, y_shuffle)
     rv = N.t5(residual, y_shuffle) if residual is not None else None
     mv = N.t5(mask, y_shuffle) if mask is not None else None
-    rc = lib.vsrk_conv_fwd(C.byref(d), C.byref(xv), wp.data_ptr(), N.ptr(bias), N.ptr(pro_scale),
-                           N.ptr(pro_shift), C.byref(rv) if rv is not None else None,
-                           C.byref(mv) if mv is not None else None, C.byref(yv), N.stream_ptr(x.device))
+    def launch():
+        return lib.vsrk_conv_fwd(C.byref(d), C.byref(xv), wp.data_ptr(), N.ptr(bias), N.ptr(pro_scale),
+                                 N.ptr(pro_shift), C.byref(rv) if rv is not None else None,
+                                 C.byref(mv) if mv is not None else None, C.byref(yv), N.stream_ptr(x.device))
+
+    rc = timer.wrap(("conv_fwd", tuple(k)), x, y, launch) if timer is not None else launch()
     N.check(rc, "conv_fwd")
     return y
 
@@ -101,14 +134,19 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, k, pad, dw: torch.Tensor, dbia
     assert dw.dtype == torch.float32 and dw.is_contiguous()
     nbytes = lib.vsrk_conv_wgrad_workspace_size(C.byref(d), C.byref(xv), C.byref(gv))
     ws = workspace(nbytes, x.device)
-    rc = lib.vsrk_conv_wgrad(C.byref(d), C.byref(xv), C.byref(gv), N.ptr(pro_scale), N.ptr(pro_shift),
-                             float(dy_scale), perm_r, dw.data_ptr(), N.ptr(dbias), 1 if accumulate else 0,
-                             ws.data_ptr(), ws.numel(), N.stream_ptr(x.device))
+    def launch():
+        return lib.vsrk_conv_wgrad(C.byref(d), C.byref(xv), C.byref(gv), N.ptr(pro_scale), N.ptr(pro_shift),
+                                   float(dy_scale), perm_r, dw.data_ptr(), N.ptr(dbias), 1 if accumulate else 0,
+                                   ws.data_ptr(), ws.numel(), N.stream_ptr(x.device))
+
+    rc = timer.wrap(("conv_wgrad", tuple(k)), x, dy, launch) if timer is not None else launch()
     N.check(rc, "conv_wgrad")
 
 
 def to_view(src: torch.Tensor, dtype: torch.dtype, cpad: int | None = None) -> torch.Tensor:
-    """(N, C, [D,] H, W) fp32 -> channels-last (N, D, H, W, cpad) in dtype (zero padded)."""
+    """(N, C, [D,] H, W) fp32 -> channels-last (N, D, H, W, cpad) in dtype (zero padded).
+    Slice [..., :C] of a padded result for a C-channel view the kernels can
+    still read in whole 16-byte chunks."""
     lib = _lib()
     if src.dim() == 4:
         n, c, h, w = src.shape

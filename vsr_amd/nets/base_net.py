@@ -21,6 +21,23 @@ class BaseNet(nn.Module):
     def __init__(self):
         super().__init__()
         self.compute_dtype = torch.bfloat16
+        self._grad_sink = None  # vsr_amd.ddp.GradSync when data-parallel
+
+    # -- gradient plumbing used by the subclasses' backward passes ----------
+    def _grad_buffer(self, p: torch.Tensor) -> torch.Tensor:
+        """fp32 tensor the wgrad kernel writes p's gradient into (a slice of a
+        communication bucket when data-parallel)."""
+        if self._grad_sink is not None:
+            return self._grad_sink.view(p)
+        return torch.empty_like(p, dtype=torch.float32)
+
+    def _grad_done(self, grads: dict, p: torch.Tensor, g: torch.Tensor) -> None:
+        """Record p's finished gradient; with a sink this may launch its bucket's
+        all-reduce right away (overlapping the rest of the backward pass)."""
+        if self._grad_sink is not None:
+            self._grad_sink.ready(p)
+        else:
+            grads[id(p)] = g
 
     def set_precision(self, precision: str) -> "BaseNet":
         """'bf16' (bf16 activations, fp32 master weights/accumulation) or 'fp32'."""

@@ -89,7 +89,7 @@ class EDSRNet(BaseNet):
         b, cin, h, w = x.shape
         f = self.num_features
         new = lambda hh, ww, c: torch.empty((b, 1, hh, ww, c), dtype=cd, device=dev)  # noqa: E731
-        xv = F.to_view(x, cd)
+        xv = F.to_view(x, cd, cpad=8)[..., :cin]  # chunk-aligned storage for the 1-channel input
         head = self.head[0]
         h0 = F.conv(xv, F.pack_weight(head.weight, 0, cd), new(h, w, f), K3, P1, bias=head.bias)
         saved = []
@@ -133,11 +133,11 @@ class EDSRNet(BaseNet):
         grads: dict = {}
 
         def wgrad(conv, x, dy, **kw):
-            dw = torch.empty_like(conv.weight)
-            db = torch.empty_like(conv.bias)
+            dw = self._grad_buffer(conv.weight)
+            db = self._grad_buffer(conv.bias)
             F.conv_wgrad(x, dy, K3, P1, dw.view(*dw.shape[:2], 1, *dw.shape[2:]), db, **kw)
-            grads[id(conv.weight)] = dw
-            grads[id(conv.bias)] = db
+            self._grad_done(grads, conv.weight, dw)
+            self._grad_done(grads, conv.bias, db)
 
         def dgrad(conv, dy, out, perm_r=1, **kw):
             return F.conv(dy, F.pack_weight(conv.weight, 1, cd, perm_r=perm_r), out, K3, P1, **kw)
@@ -145,7 +145,7 @@ class EDSRNet(BaseNet):
         # tail conv
         u = tape["tail_in"]
         hh, ww = u.shape[2], u.shape[3]
-        g = F.to_view(gy, cd)  # (b,1,H,W,out)
+        g = F.to_view(gy, cd, cpad=8)[..., :self.out_channels]  # (b,1,H,W,out), chunk-aligned storage
         tc = self.tail.conv
         wgrad(tc, u, g)
         du = dgrad(tc, g, torch.empty((b, 1, hh, ww, f), dtype=cd, device=dev))
