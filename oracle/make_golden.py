@@ -97,6 +97,7 @@ def run_case(name, spec):
     assert list(rsd) == list(msd), f"{name}: state_dict keys differ"
     for k in rsd:
         assert torch.equal(rsd[k], msd[k]), f"{name}: init of {k} differs"
+    init_sum = {k: float(v.double().sum()) for k, v in msd.items() if v.is_floating_point()}
     g = torch.Generator().manual_seed(SEED + 1)
     lr, hr = _inputs(kind, shape, r, g)
     outs, grads, losses = [], [], []
@@ -122,7 +123,7 @@ def run_case(name, spec):
     out = o_mine
     fx = {
         "name": name, "class": clsname, "kwargs": kwargs, "seed": SEED, "kind": kind,
-        "param_sum": {k: float(v.double().sum()) for k, v in msd.items() if v.is_floating_point()},
+        "param_sum": init_sum,
         "lr": lr, "hr": hr,
         "output": [o.detach() for o in out] if isinstance(out, list) else out.detach(),
         "loss_l1": float(losses[1]),
