@@ -145,6 +145,48 @@ int vsrk_psnr(const float* out, const float* target, int32_t batch, int64_t per_
               float mean, float std, float max_value, float* psnr_per_sample, float* psnr_mean, void* workspace,
               size_t workspace_bytes, void* stream);
 
+/* BatchNorm3d, training statistics (duf_net.py:116,198,201,209,212).  Split
+ * so a data-parallel caller can all-reduce the per-channel sums between the
+ * calls (SyncBatchNorm):
+ *   vsrk_bn_stats:    sum, sumsq over every voxel of x (channels-last view)
+ *   vsrk_bn_finalize: mean, biased var -> scale = gamma*invstd,
+ *                     shift = beta - mean*scale (the fused conv prologue's
+ *                     VSRK_PRO_AFFINE_RELU operands), running stats updated
+ *                     with momentum and the unbiased variance (torch semantics)
+ *   vsrk_bn_fold_running: eval mode (running statistics)
+ * Backward of BN followed by ReLU, given dz = dL/d relu(bn(x)):
+ *   vsrk_bn_relu_bwd_reduce: sum_dy, sum_dy_xhat (= dbeta, dgamma)
+ *   vsrk_bn_relu_bwd_apply:  dx [+]= gamma*invstd*(dy - sum_dy/M - xhat*sum_dy_xhat/M)
+ * Workspace: vsrk_bn_workspace_size(channels) bytes. */
+size_t vsrk_bn_workspace_size(int32_t channels);
+int vsrk_bn_stats(const vsrk_tensor5* x, float* sum, float* sumsq, void* workspace, size_t workspace_bytes,
+                  void* stream);
+int vsrk_bn_finalize(const float* sum, const float* sumsq, double count, const float* gamma, const float* beta,
+                     float eps, float momentum, float* running_mean, float* running_var, float* scale,
+                     float* shift, float* mean, float* invstd, int32_t channels, void* stream);
+int vsrk_bn_fold_running(const float* gamma, const float* beta, const float* running_mean,
+                         const float* running_var, float eps, float* scale, float* shift, int32_t channels,
+                         void* stream);
+int vsrk_bn_relu_bwd_reduce(const vsrk_tensor5* x, const vsrk_tensor5* dz, const float* scale, const float* shift,
+                            const float* mean, const float* invstd, float* sum_dy, float* sum_dy_xhat,
+                            void* workspace, size_t workspace_bytes, void* stream);
+int vsrk_bn_relu_bwd_apply(const vsrk_tensor5* x, const vsrk_tensor5* dz, const float* scale, const float* shift,
+                           const float* mean, const float* invstd, const float* gamma, const float* sum_dy,
+                           const float* sum_dy_xhat, double count, const vsrk_tensor5* dx, int32_t accumulate,
+                           void* stream);
+
+/* DUF dynamic upsampling (duf_net.py:67-97), fused: softmax over the k*k taps
+ * of per-pixel logits (n, h, w, k*k*r*r) fp32 (tap-major, as the reference's
+ * reshape), unfold of the centre frame x (n, h, w) fp32 with zero padding,
+ * contraction, pixel shuffle and residual (n, h, w, r*r) add ->
+ * out (n, r*h, r*w) fp32.  Backward writes d logits and d residual in
+ * grad_dtype (x gets no gradient: it is input data). */
+int vsrk_duf_dynfilter_fwd(const float* x, const float* logits, const float* residual, int32_t n, int32_t h,
+                           int32_t w, int32_t size_filter, int32_t upscale, float* out, void* stream);
+int vsrk_duf_dynfilter_bwd(const float* x, const float* logits, const float* grad_out, int32_t n, int32_t h,
+                           int32_t w, int32_t size_filter, int32_t upscale, void* grad_logits, void* grad_residual,
+                           int32_t grad_dtype, void* stream);
+
 const char* vsrk_last_error(void);
 const char* vsrk_version(void);
 

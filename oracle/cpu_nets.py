@@ -154,7 +154,7 @@ class DUFRef(nn.Module):
         filt = self.filterNet(feats)
         filt = filt.reshape(filt.shape[0], k * k, r * r, *filt.shape[2:])
         filt = torch.softmax(filt, dim=1)[:, :, :, 0]  # (N, k*k, r*r, H, W)
-        eye = torch.FloatTensor(np.reshape(np.eye(k * k), (k * k, 1, k, k))).to(filt.device)
+        eye = torch.FloatTensor(np.reshape(np.eye(k * k), (k * k, 1, k, k))).to(filt.device, target.dtype)
         outs = []
         for c in range(target.shape[1]):
             patches = Fn.conv2d(target[:, c], eye, padding=k // 2)          # (N, k*k, H, W)

@@ -121,6 +121,34 @@ def run_case(name, spec):
     # running stats after one train step (BatchNorm, DUF)
     buffers = {k: v.clone() for k, v in mine.state_dict().items() if "running" in k}
     out = o_mine
+    # fp64 evaluation of the restatement: the accuracy yardstick.  A parity
+    # test holds an fp32 implementation to (a multiple of) the reference's own
+    # fp32 error against this.
+    torch.manual_seed(SEED)
+    m64 = mine_cls(**kwargs).double().train()
+    lr64 = [x.double() for x in lr] if isinstance(lr, list) else lr.double()
+    hr64 = [x.double() for x in hr] if isinstance(hr, list) else hr.double()
+    out64 = m64(lr64)
+    _loss(out64, hr64).backward()
+    g64 = {k: p.grad.detach().clone() for k, p in m64.named_parameters()}
+    flat = lambda o: torch.cat([t.flatten() for t in o]) if isinstance(o, list) else o.flatten()  # noqa: E731
+    gmax = max(v.norm().item() for v in g64.values())
+    # the reference's fp32 error scale: worst over several summation orders
+    # (CPU thread counts), so an ill-conditioned gradient is not judged by
+    # one lucky sample
+    out_err32, ref32_err = 0.0, {k: (0.0 if v.norm().item() > 1e-9 * gmax else None) for k, v in g64.items()}
+    nthreads = torch.get_num_threads()
+    for nt in (1, 2, 4, nthreads):
+        torch.set_num_threads(nt)
+        torch.manual_seed(SEED)
+        m32 = mine_cls(**kwargs).train()
+        o32 = m32(lr)
+        _loss(o32, hr).backward()
+        out_err32 = max(out_err32, (flat(o32).double() - flat(out64).detach()).abs().max().item())
+        for k, p in m32.named_parameters():
+            if ref32_err[k] is not None:
+                ref32_err[k] = max(ref32_err[k], (p.grad.double() - g64[k]).norm().item() / g64[k].norm().item())
+    torch.set_num_threads(nthreads)
     fx = {
         "name": name, "class": clsname, "kwargs": kwargs, "seed": SEED, "kind": kind,
         "param_sum": init_sum,
@@ -132,12 +160,19 @@ def run_case(name, spec):
         "grad_sum": {k: float(v.double().sum()) for k, v in grads[1].items()},
         "grad_full": {k: v for k, v in grads[1].items() if v.numel() <= FULL_GRAD_MAX},
         "running_stats": buffers,
+        "output64": [o.detach() for o in out64] if isinstance(out64, list) else out64.detach(),
+        "out_err32": out_err32,
+        "grad_norm64": {k: v.norm().item() for k, v in g64.items()},
+        "grad_full64": {k: v for k, v in g64.items() if v.numel() <= FULL_GRAD_MAX},
+        "ref32_err": ref32_err,
+        "grad_max64": gmax,
     }
     OUT.mkdir(parents=True, exist_ok=True)
     torch.save(fx, OUT / f"{name}.pt")
     size = os.path.getsize(OUT / f"{name}.pt")
+    worst = max(v for v in ref32_err.values() if v is not None)
     print(f"{name}: restatement == reference (bitwise), loss={fx['loss_l1']:.6f} psnr={fx['psnr_acdc']:.4f} "
-          f"fixture {size / 1024:.0f} KiB")
+          f"fp32-vs-fp64: out {out_err32:.1e}, worst grad {worst:.1e}; fixture {size / 1024:.0f} KiB")
 
 
 def run_metrics():

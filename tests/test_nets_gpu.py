@@ -1,16 +1,29 @@
-"""End-to-end parity of the fused generators against the golden fixtures made
-from the reference itself (oracle/make_golden.py): same seed -> same initial
-weights (checked), then forward output, L1 loss, PSNR and every parameter
-gradient through the HIP path.
+"""End-to-end parity of the fused generators against golden fixtures made from
+the reference itself (oracle/make_golden.py): same seed -> same initial
+weights (checked), then forward output, L1 loss, PSNR, BatchNorm running
+statistics and every parameter gradient through the HIP path.
 
-Tolerances: fp32 path: output max |d| <= 1e-4 (normalized units),
-gradient rel-L2 <= 1e-4 per parameter; bf16 path: output max |d| <= 3e-2,
-mean |d| <= 3e-3; PSNR within 0.01 dB for both.  bf16 gradients (§8d states
-no bound) are held to rel-L2 <= 8e-2: every layer stores its activation and
-data-gradient in bf16 (2^-9 relative rounding), which over the ~35 layers of
-EDSR random-walks to the measured 3-4.5 %.  bf16 bias gradients are sums of
-B*H*W per-voxel terms with heavy cancellation, so their relative error is
-larger (measured up to 8.8 %): held to rel-L2 <= 0.15.
+Yardstick: an fp64 evaluation of the (bitwise-pinned) CPU restatement.  The
+fixture records how far the reference's own fp32 CPU path is from it
+(out_err32, ref32_err[param]); on small inputs DUF's gradients are
+ill-conditioned (BatchNorm over few voxels) and the fp32 reference itself is
+up to 1e-2 away, while EDSR's is ~1e-6.
+
+fp32 HIP path: output max |d| <= max(1e-4, 3*out_err32); gradient rel-L2 <=
+  max(1e-4, 3*ref32_err, 0.05*max_p ref32_err) per parameter (SURVEY §8d's
+  1e-4 wherever the reference itself is that accurate; the last term is the
+  net-wide conditioning: a parameter upstream of an ill-conditioned one sees
+  its ReLU masks / BatchNorm statistics perturbed at the same scale even when
+  the reference's own thread-count variation happens not to reach it).  The
+  BN and dynamic-filter kernels alone are checked at 1e-5..1e-4 against fp64
+  in test_bn_duf_kernels_gpu.py; parameters whose exact gradient is 0
+  (conv biases feeding a BatchNorm) |g| <= 1e-4 * max gradient norm.
+bf16 HIP path: output max |d| <= 3e-2, mean |d| <= 3e-3; gradient rel-L2 <=
+  max(8e-2, 3*ref32_err) (0.15 for biases and BatchNorm affine parameters:
+  global sums with cancellation); zero-gradient parameters <= 2e-2 * max norm.
+  Every layer stores activations and data-gradients in bf16 (2^-9 relative
+  rounding), which over ~35 layers random-walks to the measured few %.
+PSNR within 0.01 dB of the reference's fp32 PSNR for both.
 """
 import pytest
 import torch
@@ -56,7 +69,7 @@ def _psnr(out, hr):
     return psnr_denorm(out, hr, "acdc")
 
 
-CASES = ["edsr_x4_small", "edsr_x3_small", "edsr_x2_cfg1", "edsr_x4_canon"]
+CASES = ["edsr_x4_small", "edsr_x3_small", "edsr_x2_cfg1", "edsr_x4_canon", "duf_x4_canon"]
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
@@ -69,20 +82,35 @@ def test_net_matches_golden(name, precision):
     loss = _l1(out, hr)
     loss.backward()
     torch.cuda.synchronize()
-    got, exp = _flat(out).detach().cpu().double(), _flat(fx["output"]).double()
+    got, exp = _flat(out).detach().cpu().double(), _flat(fx["output64"]).double()
     d = (got - exp).abs()
     if precision == "fp32":
-        assert d.max().item() <= 1e-4, d.max().item()
+        assert d.max().item() <= max(1e-4, 3 * fx["out_err32"]), d.max().item()
     else:
         assert d.max().item() <= 3e-2 and d.mean().item() <= 3e-3, (d.max().item(), d.mean().item())
     assert abs(_psnr([o.detach() for o in out] if isinstance(out, list) else out.detach(), hr).item()
                - fx["psnr_acdc"]) <= 0.01
+    for key, ref in fx["running_stats"].items():  # BatchNorm running statistics after the step
+        got_rs = net.state_dict()[key].detach().cpu().double()
+        assert (got_rs - ref.double()).abs().max().item() <= (1e-5 if precision == "fp32" else 2e-2) * (
+            1 + ref.double().abs().max().item()), key
+    gmax = fx["grad_max64"]
+    net_r32 = max(v for v in fx["ref32_err"].values() if v is not None)
     for k, p in net.named_parameters():
-        tol = 1e-4 if precision == "fp32" else (0.15 if k.endswith("bias") else 8e-2)
-        gn = fx["grad_norm"][k]
-        if k in fx["grad_full"]:
-            ref = fx["grad_full"][k].double()
-            rel = (p.grad.detach().cpu().double() - ref).norm().item() / max(ref.norm().item(), 1e-12)
+        g = p.grad.detach().cpu().double()
+        r32 = fx["ref32_err"][k]
+        if r32 is None:  # exact gradient is zero
+            assert g.norm().item() <= (1e-4 if precision == "fp32" else 2e-2) * gmax, (k, g.norm().item())
+            continue
+        if k in fx["grad_full64"]:
+            ref = fx["grad_full64"][k].double()
+            rel = (g - ref).norm().item() / ref.norm().item()
         else:
-            rel = abs(p.grad.double().norm().item() - gn) / max(gn, 1e-12)
-        assert rel <= tol, (k, rel)
+            n64 = fx["grad_norm64"][k]
+            rel = abs(g.norm().item() - n64) / n64
+        is_bn = ".bn" in k
+        if precision == "fp32":
+            tol = max(1e-4, 3 * r32, 0.05 * net_r32)
+        else:
+            tol = max(0.15 if (k.endswith("bias") or is_bn) else 8e-2, 3 * r32)
+        assert rel <= tol, (k, rel, tol)

@@ -1,0 +1,65 @@
+"""Standalone timing of the conv kernels at the cfg-2 shapes (for rocprofv3
+--pmc passes and A/B work).  Prints one line per case: mean ms and TFLOP/s."""
+import argparse
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from vsr_amd import _native  # noqa: E402
+from vsr_amd import functional as F  # noqa: E402
+
+CASES = {
+    # name: (N, D, H, W, Cin, Cout, k, pad)
+    "edsr3x3": (64, 1, 128, 128, 64, 64, (1, 3, 3), (0, 1, 1)),
+    "duf3x3x3": (4, 16, 128, 128, 64, 32, (3, 3, 3), (1, 1, 1)),
+    "duf1x1x1": (64, 7, 128, 128, 128, 128, (1, 1, 1), (0, 0, 0)),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--case", default="edsr3x3")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--what", default="fwd,res,wgrad")
+    args = ap.parse_args()
+    _native.load()
+    dev = "cuda"
+    n, d, h, w, ci, co, k, pad = CASES[args.case]
+    dt = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.randn((n, d, h, w, ci), generator=g).to(dev, dt)
+    wt = (torch.randn((co, ci, *k), generator=g) * 0.05).to(dev)
+    b = torch.randn(co, generator=g).to(dev)
+    do = d + 2 * pad[0] - k[0] + 1
+    y = torch.empty((n, do, h, w, co), dtype=dt, device=dev)
+    res = torch.randn((n, do, h, w, co), generator=g).to(dev, dt)
+    gy = torch.randn((n, do, h, w, co), generator=g).to(dev, dt)
+    dw = torch.empty((co, ci, *k), device=dev)
+    db = torch.empty(co, device=dev)
+    wp = F.pack_weight(wt, 0, dt)
+    flop = 2.0 * n * do * h * w * co * ci * k[0] * k[1] * k[2]
+    cases = {
+        "fwd": lambda: F.conv(x, wp, y, k, pad, bias=b),
+        "res": lambda: F.conv(x, wp, y, k, pad, bias=b, out_scale=0.1, residual=res),
+        "wgrad": lambda: F.conv_wgrad(x, gy, k, pad, dw, db),
+    }
+    for name in args.what.split(","):
+        fn = cases[name]
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(args.iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / args.iters
+        print(f"{args.case:10s} {name:6s} {ms * 1e3:9.1f} us  {flop / ms / 1e9:8.1f} TFLOP/s  "
+              f"({flop / ms / 1e9 / 2500 * 100:.1f}% of 2.5 PF)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,314 @@
+// BatchNorm3d (training statistics) around the fused BN+ReLU conv prologue.
+//
+// Replaces nn.BatchNorm3d + nn.ReLU of the DUF dense blocks and tail
+// (duf_net.py:116-118,195-214).  The normalisation itself is never
+// materialised: the forward folds (gamma, beta, batch mean, batch var) into a
+// per-channel (scale, shift) that the consuming conv applies while staging its
+// input (VSRK_PRO_AFFINE_RELU).  Backward recomputes the pre-ReLU value from x.
+//
+// Reductions are channels-last: each thread owns one 16-byte chunk position
+// (8 bf16 / 4 fp32 channels) of a run of voxels and accumulates in registers;
+// the per-block partials are reduced in a fixed order in double precision
+// (deterministic, and robust for sum-of-squares variance).
+#include "vsrk_common.h"
+#include "vsrk_internal.h"
+
+namespace {
+
+constexpr int RB = 512;  // reduction blocks (partials)
+
+__device__ __forceinline__ void decode_voxel(int64_t v, const View& t, int& n, int& d, int& h, int& w) {
+  w = v % t.w;
+  v /= t.w;
+  h = v % t.h;
+  v /= t.h;
+  d = v % t.d;
+  n = v / t.d;
+}
+
+// modes: 0 = sum x, sum x^2 (stats); 1 = sum dy, sum dy*xhat with
+// dy = dz * (x*scale + shift > 0) (BN+ReLU backward)
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void chan_reduce_kernel(View x, View dz, const float* __restrict__ scale,
+                                                          const float* __restrict__ shift,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, int64_t nvox,
+                                                          float* __restrict__ part) {
+  constexpr int E = Chunk<T>::E;
+  const int C = x.c;
+  const int cpv = (C + E - 1) / E;  // chunks per voxel
+  const int vpb = blockDim.x / cpv; // voxels per block iteration (blockDim is a multiple of cpv)
+  const int ch = threadIdx.x % cpv, vl = threadIdx.x / cpv;
+  const int c0 = ch * E;
+  float s1[E], s2[E], sc[E], sh[E], mu[E], is[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    s1[e] = 0.f;
+    s2[e] = 0.f;
+    const int c = min(c0 + e, C - 1);
+    if (MODE == 1) {
+      sc[e] = scale[c];
+      sh[e] = shift[c];
+      mu[e] = mean[c];
+      is[e] = invstd[c];
+    }
+  }
+  if (vl < vpb) {
+    const int64_t per = (nvox + gridDim.x - 1) / gridDim.x;
+    const int64_t v0 = blockIdx.x * per, v1 = min(nvox, v0 + per);
+    for (int64_t v = v0 + vl; v < v1; v += vpb) {
+      int n, d, h, w;
+      decode_voxel(v, x, n, d, h, w);
+      float f[E];
+      const T* px = reinterpret_cast<const T*>(x.ptr) + view_off(x, n, d, h, w, c0);
+      if (c0 + E <= C) {
+        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(px), f);
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) f[e] = c0 + e < C ? to_f32<T>(px[e]) : 0.f;
+      }
+      if (MODE == 0) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          s1[e] += f[e];
+          s2[e] = fmaf(f[e], f[e], s2[e]);
+        }
+      } else {
+        float g[E];
+        const T* pg = reinterpret_cast<const T*>(dz.ptr) + view_off(dz, n, d, h, w, c0);
+        if (c0 + E <= C) {
+          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(pg), g);
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e) g[e] = c0 + e < C ? to_f32<T>(pg[e]) : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float dy = fmaf(f[e], sc[e], sh[e]) > 0.f ? g[e] : 0.f;
+          s1[e] += dy;
+          s2[e] = fmaf(dy, (f[e] - mu[e]) * is[e], s2[e]);
+        }
+      }
+    }
+  }
+  // block reduce over the vpb voxel lanes of each chunk position (fixed order)
+  __shared__ float red[2][256 * 8];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    red[0][threadIdx.x * E + e] = s1[e];
+    red[1][threadIdx.x * E + e] = s2[e];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < cpv * E; i += blockDim.x) {
+    const int chk = i / E, e = i % E;
+    float a = 0.f, b = 0.f;
+    for (int k = 0; k < vpb; ++k) {
+      a += red[0][(k * cpv + chk) * E + e];
+      b += red[1][(k * cpv + chk) * E + e];
+    }
+    const int c = chk * E + e;
+    if (c < C) {
+      part[((int64_t)blockIdx.x * 2) * C + c] = a;
+      part[((int64_t)blockIdx.x * 2 + 1) * C + c] = b;
+    }
+  }
+}
+
+__global__ void chan_final_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ o1,
+                                  float* __restrict__ o2) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, b = 0.0;
+  for (int k = 0; k < nblk; ++k) {
+    a += part[((int64_t)k * 2) * C + c];
+    b += part[((int64_t)k * 2 + 1) * C + c];
+  }
+  o1[c] = (float)a;
+  o2[c] = (float)b;
+}
+
+__global__ void bn_finalize_kernel(const float* __restrict__ sum, const float* __restrict__ sumsq, double count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                                   float momentum, float* __restrict__ rmean, float* __restrict__ rvar,
+                                   float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ mean,
+                                   float* __restrict__ invstd, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double m = (double)sum[c] / count;
+  double var = (double)sumsq[c] / count - m * m;
+  if (var < 0) var = 0;
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale[c] = g * is;
+  shift[c] = b - (float)m * g * is;
+  mean[c] = (float)m;
+  invstd[c] = is;
+  if (rmean && rvar) {  // running stats: momentum update, unbiased variance (torch semantics)
+    const double uvar = count > 1 ? var * count / (count - 1) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)m;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)uvar;
+  }
+}
+
+// eval mode: fold running statistics
+__global__ void bn_fold_running_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                       const float* __restrict__ rmean, const float* __restrict__ rvar, float eps,
+                                       float* __restrict__ scale, float* __restrict__ shift, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float is = 1.f / sqrtf(rvar[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale[c] = g * is;
+  shift[c] = b - rmean[c] * g * is;
+}
+
+// dx [+]= gamma*invstd*(dy - sum_dy/M - xhat*sum_dy_xhat/M), dy = dz*(x*scale+shift > 0)
+template <typename T>
+__global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(View x, View dz, View dx,
+                                                                const float* __restrict__ scale,
+                                                                const float* __restrict__ shift,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ invstd,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ sdy,
+                                                                const float* __restrict__ sdyx, float inv_count,
+                                                                int64_t nchunks, int accumulate) {
+  constexpr int E = Chunk<T>::E;
+  const int C = x.c;
+  const int cpv = (C + E - 1) / E;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nchunks;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int ch = i % cpv;
+    const int64_t v = i / cpv;
+    int n, d, h, w;
+    decode_voxel(v, x, n, d, h, w);
+    const int c0 = ch * E;
+    const bool full = c0 + E <= C;
+    float f[E], g[E], o[E];
+    const T* px = reinterpret_cast<const T*>(x.ptr) + view_off(x, n, d, h, w, c0);
+    const T* pg = reinterpret_cast<const T*>(dz.ptr) + view_off(dz, n, d, h, w, c0);
+    T* po = reinterpret_cast<T*>(dx.ptr) + view_off(dx, n, d, h, w, c0);
+    if (full) {
+      Chunk<T>::unpack(*reinterpret_cast<const uint4*>(px), f);
+      Chunk<T>::unpack(*reinterpret_cast<const uint4*>(pg), g);
+      if (accumulate) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(po), o);
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const bool ok = c0 + e < C;
+        f[e] = ok ? to_f32<T>(px[e]) : 0.f;
+        g[e] = ok ? to_f32<T>(pg[e]) : 0.f;
+        o[e] = (ok && accumulate) ? to_f32<T>(po[e]) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int c = min(c0 + e, C - 1);
+      const float dy = fmaf(f[e], scale[c], shift[c]) > 0.f ? g[e] : 0.f;
+      const float xh = (f[e] - mean[c]) * invstd[c];
+      const float gm = gamma ? gamma[c] : 1.f;
+      float r = gm * invstd[c] * (dy - sdy[c] * inv_count - xh * sdyx[c] * inv_count);
+      if (accumulate) r += o[e];
+      o[e] = r;
+    }
+    if (full) {
+      *reinterpret_cast<uint4*>(po) = Chunk<T>::pack(o);
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (c0 + e < C) po[e] = from_f32<T>(o[e]);
+    }
+  }
+}
+
+int reduce_launch(int mode, const vsrk_tensor5* x, const vsrk_tensor5* dz, const float* scale, const float* shift,
+                  const float* mean, const float* invstd, float* o1, float* o2, void* ws, size_t ws_bytes,
+                  hipStream_t s) {
+  const int E = x->dtype == VSRK_BF16 ? 8 : 4;
+  const int cpv = ceil_div(x->c, E);
+  VSRK_CHECK(cpv <= 256, "bn: too many channels (%d)", x->c);
+  const int vpb = 256 / cpv;
+  const int64_t nv = (int64_t)x->n * x->d * x->h * x->w;
+  const int nblk = (int)std::min<int64_t>(RB, std::max<int64_t>(1, ceil_div64(nv, 64)));
+  const size_t need = (size_t)nblk * 2 * x->c * sizeof(float);
+  VSRK_CHECK(ws && ws_bytes >= need, "bn: workspace %zu < %zu bytes", ws_bytes, need);
+  View vx = make_view(x);
+  View vg = dz ? make_view(dz) : vx;
+  float* part = (float*)ws;
+  const int thr = cpv * vpb;
+  if (x->dtype == VSRK_BF16) {
+    if (mode == 0) chan_reduce_kernel<bf16, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nv, part);
+    else chan_reduce_kernel<bf16, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nv, part);
+  } else {
+    if (mode == 0) chan_reduce_kernel<float, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nv, part);
+    else chan_reduce_kernel<float, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nv, part);
+  }
+  VSRK_LAUNCH_CHECK("bn_reduce");
+  chan_final_kernel<<<ceil_div(x->c, 256), 256, 0, s>>>(part, nblk, x->c, o1, o2);
+  VSRK_LAUNCH_CHECK("bn_reduce_final");
+  return VSRK_OK;
+}
+
+}  // namespace
+
+extern "C" size_t vsrk_bn_workspace_size(int32_t channels) { return (size_t)RB * 2 * channels * sizeof(float); }
+
+extern "C" int vsrk_bn_stats(const vsrk_tensor5* x, float* sum, float* sumsq, void* workspace,
+                             size_t workspace_bytes, void* stream) {
+  VSRK_CHECK(x && x->ptr && sum && sumsq, "bn_stats: null argument");
+  return reduce_launch(0, x, nullptr, nullptr, nullptr, nullptr, nullptr, sum, sumsq, workspace, workspace_bytes,
+                       (hipStream_t)stream);
+}
+
+extern "C" int vsrk_bn_finalize(const float* sum, const float* sumsq, double count, const float* gamma,
+                                const float* beta, float eps, float momentum, float* running_mean,
+                                float* running_var, float* scale, float* shift, float* mean, float* invstd,
+                                int32_t channels, void* stream) {
+  VSRK_CHECK(sum && sumsq && scale && shift && mean && invstd && count > 0, "bn_finalize: bad argument");
+  bn_finalize_kernel<<<ceil_div(channels, 256), 256, 0, (hipStream_t)stream>>>(
+      sum, sumsq, count, gamma, beta, eps, momentum, running_mean, running_var, scale, shift, mean, invstd, channels);
+  VSRK_LAUNCH_CHECK("bn_finalize");
+  return VSRK_OK;
+}
+
+extern "C" int vsrk_bn_fold_running(const float* gamma, const float* beta, const float* running_mean,
+                                    const float* running_var, float eps, float* scale, float* shift,
+                                    int32_t channels, void* stream) {
+  VSRK_CHECK(running_mean && running_var && scale && shift, "bn_fold_running: null argument");
+  bn_fold_running_kernel<<<ceil_div(channels, 256), 256, 0, (hipStream_t)stream>>>(
+      gamma, beta, running_mean, running_var, eps, scale, shift, channels);
+  VSRK_LAUNCH_CHECK("bn_fold_running");
+  return VSRK_OK;
+}
+
+extern "C" int vsrk_bn_relu_bwd_reduce(const vsrk_tensor5* x, const vsrk_tensor5* dz, const float* scale,
+                                       const float* shift, const float* mean, const float* invstd, float* sum_dy,
+                                       float* sum_dy_xhat, void* workspace, size_t workspace_bytes, void* stream) {
+  VSRK_CHECK(x && dz && scale && shift && mean && invstd && sum_dy && sum_dy_xhat, "bn_relu_bwd_reduce: null");
+  VSRK_CHECK(x->dtype == dz->dtype && x->c == dz->c, "bn_relu_bwd_reduce: x/dz mismatch");
+  return reduce_launch(1, x, dz, scale, shift, mean, invstd, sum_dy, sum_dy_xhat, workspace, workspace_bytes,
+                       (hipStream_t)stream);
+}
+
+extern "C" int vsrk_bn_relu_bwd_apply(const vsrk_tensor5* x, const vsrk_tensor5* dz, const float* scale,
+                                      const float* shift, const float* mean, const float* invstd,
+                                      const float* gamma, const float* sum_dy, const float* sum_dy_xhat,
+                                      double count, const vsrk_tensor5* dx, int32_t accumulate, void* stream) {
+  VSRK_CHECK(x && dz && dx && scale && shift && mean && invstd && sum_dy && sum_dy_xhat, "bn_relu_bwd_apply: null");
+  VSRK_CHECK(x->dtype == dz->dtype && x->dtype == dx->dtype && x->c == dz->c && x->c == dx->c,
+             "bn_relu_bwd_apply: view mismatch");
+  const int E = x->dtype == VSRK_BF16 ? 8 : 4;
+  const int64_t nchunks = (int64_t)x->n * x->d * x->h * x->w * ceil_div(x->c, E);
+  const int grid = (int)std::min<int64_t>(8192, ceil_div64(nchunks, 256));
+  hipStream_t s = (hipStream_t)stream;
+  if (x->dtype == VSRK_BF16)
+    bn_relu_bwd_apply_kernel<bf16><<<grid, 256, 0, s>>>(make_view(x), make_view(dz), make_view(dx), scale, shift,
+                                                        mean, invstd, gamma, sum_dy, sum_dy_xhat,
+                                                        (float)(1.0 / count), nchunks, accumulate);
+  else
+    bn_relu_bwd_apply_kernel<float><<<grid, 256, 0, s>>>(make_view(x), make_view(dz), make_view(dx), scale, shift,
+                                                         mean, invstd, gamma, sum_dy, sum_dy_xhat,
+                                                         (float)(1.0 / count), nchunks, accumulate);
+  VSRK_LAUNCH_CHECK("bn_relu_bwd_apply");
+  return VSRK_OK;
+}

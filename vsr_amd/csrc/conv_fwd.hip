@@ -16,10 +16,41 @@
 // channels-last stores.
 //   bf16: v_mfma_f32_32x32x16_bf16, one per 16 channels.
 //   fp32: v_mfma_f32_32x32x2_f32, four per 8 channels (exact fp32, parity path).
+#include <type_traits>
 #include "conv_common.h"
 
 namespace {
 using namespace vsrk_conv;
+
+// 4 consecutive channels of an epilogue tensor, kept packed (uint2 for bf16,
+// uint4 for fp32) between the batched loads and the stores.
+template <typename YT, typename Pk>
+__device__ __forceinline__ Pk load_pk(const char* base, int64_t off, bool vec, int valid) {
+  const YT* p = reinterpret_cast<const YT*>(base) + off;
+  if (vec) return *reinterpret_cast<const Pk*>(p);
+  Pk v;
+  YT* q = reinterpret_cast<YT*>(&v);
+  for (int e = 0; e < 4; ++e) q[e] = e < valid ? p[e] : from_f32<YT>(0.f);
+  return v;
+}
+template <typename YT, typename Pk>
+__device__ __forceinline__ void unpack_pk(Pk v, float* f) {
+  const YT* q = reinterpret_cast<const YT*>(&v);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) f[e] = to_f32<YT>(q[e]);
+}
+template <typename YT>
+__device__ __forceinline__ void unpack_pk(uint2 v, float* f) { unpack_pk<YT, uint2>(v, f); }
+template <typename YT>
+__device__ __forceinline__ void unpack_pk(uint4 v, float* f) { unpack_pk<YT, uint4>(v, f); }
+template <typename YT, typename Pk>
+__device__ __forceinline__ Pk pack_pk(const float* f) {
+  Pk v;
+  YT* q = reinterpret_cast<YT*>(&v);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) q[e] = from_f32<YT>(f[e]);
+  return v;
+}
 
 // ---------------------------------------------------------------------------
 // forward / data-gradient
@@ -36,7 +67,10 @@ using namespace vsrk_conv;
 // use) and overlaps other waves' compute.  KK is a template parameter so the
 // tap loop is straight-line code (LDS reads pipelined, rows shared by
 // neighbouring taps read once).
-template <typename T, int NT, int MS, int KK, bool VEC, typename YT>
+// XM: input addressing mode — 0 plain channels-last view (precomputed
+// offsets), 1 sub-pixel view (generic addressing), 2 element loads (views
+// that cannot be read in 16-byte chunks).
+template <typename T, int NT, int MS, int KK, int XM, typename YT>
 __global__ __launch_bounds__(NTHR) void conv_fwd_kernel(ConvArgs a) {
   constexpr int NS = NT / 32;
   constexpr int FTH = 8 * MS;  // tile rows: MS rows (of 32 voxels) per wave
@@ -54,17 +88,33 @@ __global__ __launch_bounds__(NTHR) void conv_fwd_kernel(ConvArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   char* ldsA = lds;
   char* ldsB = lds + SLOTS * ROWB;  // two buffers of BBYTES
-  float* lsc = reinterpret_cast<float*>(ldsB + 2 * BBYTES);
+  float* lbias_all = reinterpret_cast<float*>(ldsB + 2 * BBYTES);  // [cout_pad], view order
+  float* lsc = lbias_all + a.cout_pad;
   float* lsh = lsc + a.cin_pad;
   const bool relu_in = (a.prologue & VSRK_PRO_RELU) != 0;
   if (a.prologue) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, a.cin_pad, tid, NTHR);
+  for (int i = tid; i < a.cout_pad; i += NTHR) {
+    float b = 0.f;
+    if (a.bias && i < a.cout) {
+      int cb = i;
+      if (a.bias_r > 1) {  // view order (sub, c') -> torch order c'*r*r + sub
+        const int rr = a.bias_r * a.bias_r, cp = a.cout / rr;
+        const int sub = cb / cp;
+        cb = (cb - sub * cp) * rr + sub;
+      }
+      b = a.bias[cb];
+    }
+    lbias_all[i] = b;
+  }
 
   // this workgroup's tiles: XCD group x = blockIdx % 8 owns a contiguous
   // range of tiles; its workgroups take them round-robin.
   const int G = gridDim.x;
   const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
-  const int gx = (G >> 3) + (x < (G & 7) ? 1 : 0);  // workgroups in this XCD group
-  const int t_lo = (int)((int64_t)a.ntiles * x / 8), t_hi = (int)((int64_t)a.ntiles * (x + 1) / 8);
+  const int gx = (G >> 3) + (x < (G & 7) ? 1 : 0);      // workgroups in this XCD group
+  const int cx = x * (G >> 3) + min(x, G & 7);           // workgroups in groups before it
+  const int t_lo = (int)((int64_t)a.ntiles * cx / G);    // its share of tiles, by size
+  const int t_hi = (int)((int64_t)a.ntiles * (cx + gx) / G);
   const int nchunk = (a.cin + CK - 1) / CK;
 
   struct Tile {
@@ -89,62 +139,95 @@ __global__ __launch_bounds__(NTHR) void conv_fwd_kernel(ConvArgs a) {
     return tl;
   };
 
+  // Per-thread staging geometry, fixed for the launch: each owned 16-byte
+  // chunk's halo position, its element offset from the tile's corner (mode 0)
+  // and its LDS address.  Per stage only wave-uniform terms change, so the
+  // address of a chunk costs a 32->64-bit add and a select.
+  constexpr int NBJ = (NBI + 7) / 8;
+  int a_hw[MAXA], a_rel[MAXA], a_lds[MAXA], b_rel[NBJ];
+#pragma unroll
+  for (int i = 0; i < MAXA; ++i) {
+    const int q = tid + i * NTHR;
+    const int slot = q >> 2;
+    const int hh = slot / HWd, ww = slot - hh * HWd;
+    a_hw[i] = q < SLOTS * 4 ? ((hh << 8) | ww) : -1;
+    a_rel[i] = (int)(hh * a.x.sh + ww * a.x.sw) + (q & 3) * E;
+    a_lds[i] = slot * ROWB + (q & 3) * 16;
+  }
+#pragma unroll
+  for (int jj = 0; jj < NBJ; ++jj) {
+    const int row = (wave + 8 * jj) * 16 + (lane >> 2);
+    const int kc = (lane & 3) ^ ((row >> 2) & 3);
+    const int tap = row / NT, nn = row - tap * NT;
+    b_rel[jj] = (tap * a.cout_pad + nn) * a.cin_pad + kc * E;
+  }
+  const int cpart = (tid & 3) * E;  // channel offset of every owned chunk within a stage
+
   uint4 ra[MAXA];
-  unsigned okmask = 0;
+  unsigned okmask = 0, tinb = 0;
   auto issue = [&](const Tile& tl, int s, int buf) __attribute__((always_inline)) {
     const int kdi = tl.kd_lo + s / nchunk;
     const int c0 = (s % nchunk) * CK;
     const int di = tl.dz + kdi - a.pd;
-    const bool dvalid = di >= 0 && di < a.x.d;
-    okmask = 0;
+    const int hb = tl.h0 - a.ph, wb0 = tl.w0 - a.pw;  // halo corner
+    if (s == 0) {  // spatial validity of the owned chunks for this tile
+      tinb = 0;
 #pragma unroll
-    for (int i = 0; i < MAXA; ++i) {
-      const int q = tid + i * NTHR;
-      const int slot = q >> 2;
-      const int hh = slot / HWd, ww = slot - hh * HWd;
-      const int hi = tl.h0 + hh - a.ph, wi = tl.w0 + ww - a.pw;
-      const int c = c0 + (q & 3) * E;
-      const bool ok = q < SLOTS * 4 && dvalid && hi >= 0 && hi < a.x.h && wi >= 0 && wi < a.x.w && c < a.cin;
-      okmask |= (ok ? 1u : 0u) << i;
-      if constexpr (VEC) {
-        ra[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.x.ptr) +
-                                                view_off(a.x, tl.nb, ok ? di : 0, ok ? hi : 0, ok ? wi : 0,
-                                                         ok ? c : 0));
-      } else {
-        ra[i] = ok ? load_raw<T>(a.x, tl.nb, di, hi, wi, c, a.cin, false) : make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < MAXA; ++i) {
+        const int hh = a_hw[i] >> 8, ww = a_hw[i] & 0xff;
+        const bool ok = a_hw[i] >= 0 && hb + hh >= 0 && hb + hh < a.x.h && wb0 + ww >= 0 && wb0 + ww < a.x.w;
+        tinb |= (ok ? 1u : 0u) << i;
+      }
+    }
+    const bool sok = di >= 0 && di < a.x.d && c0 + cpart < a.cin;  // depth / channel validity of the stage
+    okmask = sok ? tinb : 0u;
+    if constexpr (XM == 0) {
+      const T* xb = reinterpret_cast<const T*>(a.x.ptr);
+      const T* base = xb + (tl.nb * a.x.sn + (int64_t)di * a.x.sd + (int64_t)hb * a.x.sh + (int64_t)wb0 * a.x.sw + c0);
+#pragma unroll
+      for (int i = 0; i < MAXA; ++i)
+        ra[i] = *reinterpret_cast<const uint4*>(((okmask >> i) & 1) ? base + a_rel[i] : xb);
+    } else {
+#pragma unroll
+      for (int i = 0; i < MAXA; ++i) {
+        const bool ok = (okmask >> i) & 1;
+        const int hi = hb + (a_hw[i] >> 8), wi = wb0 + (a_hw[i] & 0xff);
+        const int c = c0 + cpart;
+        if constexpr (XM == 1) {
+          ra[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.x.ptr) +
+                                                  view_off(a.x, tl.nb, ok ? di : 0, ok ? hi : 0, ok ? wi : 0,
+                                                           ok ? c : 0));
+        } else {
+          ra[i] = ok ? load_raw<T>(a.x, tl.nb, di, hi, wi, c, a.cin, false) : make_uint4(0, 0, 0, 0);
+        }
       }
     }
     // B (weights, identical for every workgroup): LDS-DMA into buffer `buf`,
     // 64-byte rows [tap*NT + n]; chunk position p of row n holds k-chunk
     // p ^ ((n>>2)&3) (swizzle applied on the source address: LDS-DMA writes
     // lane-linear) so the ds_read_b128 column slices are conflict-free.
-    const T* wb = reinterpret_cast<const T*>(a.w) + (int64_t)kdi * TAPS * a.cout_pad * a.cin_pad + c0;
+    const T* wb = reinterpret_cast<const T*>(a.w) + (int64_t)kdi * TAPS * a.cout_pad * a.cin_pad +
+                  (int64_t)tl.n0 * a.cin_pad + c0;
     char* bdst = ldsB + buf * BBYTES;
 #pragma unroll
-    for (int jj = 0; jj < (NBI + 7) / 8; ++jj) {
+    for (int jj = 0; jj < NBJ; ++jj) {
       const int gi = wave + 8 * jj;
-      if (gi < NBI) {
-        const int row = gi * 16 + (lane >> 2);
-        const int kc = (lane & 3) ^ ((row >> 2) & 3);
-        const int tap = row / NT, nn = row - tap * NT;
-        const T* src = wb + ((int64_t)tap * a.cout_pad + tl.n0 + nn) * a.cin_pad + kc * E;
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+      if (gi < NBI)
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(wb + b_rel[jj]),
                                          (void __attribute__((address_space(3)))*)(bdst + gi * 1024), 16, 0, 0);
-      }
     }
   };
   auto commit = [&](int s) __attribute__((always_inline)) {
-    const int c0 = (s % nchunk) * CK;
+    const int c = (s % nchunk) * CK + cpart;
+    const bool partial = c + E > a.cin;
 #pragma unroll
     for (int i = 0; i < MAXA; ++i) {
-      const int q = tid + i * NTHR;
-      if (q < SLOTS * 4) {
-        const int c = c0 + (q & 3) * E;
+      if (a_hw[i] >= 0) {
         uint4 v = ra[i];
-        if constexpr (VEC) v = mask_tail<T>(v, a.cin - c);
+        if (XM != 2 && partial) v = mask_tail<T>(v, a.cin - c);
         if (a.prologue) v = prologue_lds<T>(v, c, relu_in, lsc, lsh);
         if (!((okmask >> i) & 1)) v = make_uint4(0, 0, 0, 0);
-        *reinterpret_cast<uint4*>(ldsA + (q >> 2) * ROWB + (q & 3) * 16) = v;
+        *reinterpret_cast<uint4*>(ldsA + a_lds[i]) = v;
       }
     }
   };
@@ -157,69 +240,58 @@ __global__ __launch_bounds__(NTHR) void conv_fwd_kernel(ConvArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.f;
 
+  // Epilogue, per (row, 32-channel block): all of its loads (mask, residual,
+  // accumulate target; kept packed) are issued before any of its stores,
+  // since a store might alias them and would otherwise serialise one round
+  // trip per 4-channel group.
   auto epilogue = [&](const Tile& tl) __attribute__((always_inline)) {
+    using Pk = typename std::conditional<sizeof(YT) == 4, uint4, uint2>::type;
 #pragma unroll
     for (int ms = 0; ms < MS; ++ms) {
       const int ho = tl.h0 + wave * MS + ms, wo = tl.w0 + r;
-      if (ho < a.y.h && wo < a.y.w) {
+      const bool row_ok = ho < a.y.h && wo < a.y.w;
 #pragma unroll
-        for (int ns = 0; ns < NS; ++ns) {
+      for (int ns = 0; ns < NS; ++ns) {
+        Pk mv[4], rv[4], ov[4];
+        int64_t yoff[4];
+        int valid[4];
+        bool vecs[4];
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int co = tl.n0 + ns * 32 + 8 * g + 4 * hf;
-            if (co < a.cout) {
-              const int valid = min(4, a.cout - co);
-              float v[4];
+        for (int g = 0; g < 4; ++g) {
+          const int co = tl.n0 + ns * 32 + 8 * g + 4 * hf;
+          const bool ok = row_ok && co < a.cout;
+          valid[g] = ok ? min(4, a.cout - co) : 0;
+          const int64_t yo = ok ? view_off(a.y, tl.nb, tl.dz, ho, wo, co) : 0;
+          vecs[g] = (valid[g] == 4) && ((yo & 3) == 0) && ((((uintptr_t)a.y.ptr) & (4 * sizeof(YT) - 1)) == 0);
+          yoff[g] = yo;
+          if (ok) {
+            if (a.has_mask) mv[g] = load_pk<YT, Pk>(a.msk.ptr, view_off(a.msk, tl.nb, tl.dz, ho, wo, co), vecs[g], valid[g]);
+            if (a.has_res) rv[g] = load_pk<YT, Pk>(a.res.ptr, view_off(a.res, tl.nb, tl.dz, ho, wo, co), vecs[g], valid[g]);
+            if (a.accumulate) ov[g] = load_pk<YT, Pk>(a.y.ptr, yo, vecs[g], valid[g]);
+          }
+        }
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                float t = acc[ms][ns][4 * g + e];
-                if (a.bias && e < valid) {
-                  int cb = co + e;
-                  if (a.bias_r > 1) {  // view order (sub, c') -> torch order c'*r*r + sub
-                    const int rr = a.bias_r * a.bias_r, cp = a.cout / rr;
-                    const int sub = cb / cp;
-                    cb = (cb - sub * cp) * rr + sub;
-                  }
-                  t += a.bias[cb];
-                }
-                t *= a.out_scale;
-                if (a.act == VSRK_ACT_RELU) t = fmaxf(t, 0.f);
-                v[e] = t;
-              }
-              const int64_t yo = view_off(a.y, tl.nb, tl.dz, ho, wo, co);
-              const bool vec = (valid == 4) && ((yo & 3) == 0) &&
-                               ((((uintptr_t)a.y.ptr) & (4 * sizeof(YT) - 1)) == 0);
-              if (a.has_mask) {
-                float m[4];
-                load4<YT>(a.msk.ptr, view_off(a.msk, tl.nb, tl.dz, ho, wo, co), vec, valid, m);
+        for (int g = 0; g < 4; ++g) {
+          const int co = tl.n0 + ns * 32 + 8 * g + 4 * hf;
+          if (valid[g] > 0) {
+            float v[4], m[4], rr[4], o[4];
+            if (a.has_mask) unpack_pk<YT>(mv[g], m);
+            if (a.has_res) unpack_pk<YT>(rv[g], rr);
+            if (a.accumulate) unpack_pk<YT>(ov[g], o);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = m[e] > 0.f ? v[e] : 0.f;
-              }
-              if (a.has_res) {
-                float rr[4];
-                load4<YT>(a.res.ptr, view_off(a.res, tl.nb, tl.dz, ho, wo, co), vec, valid, rr);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] += rr[e];
-              }
-              if (a.accumulate) {
-                float o[4];
-                load4<YT>(a.y.ptr, yo, vec, valid, o);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] += o[e];
-              }
-              YT* yp = reinterpret_cast<YT*>(a.y.ptr) + yo;
-              if (vec) {
-                if constexpr (sizeof(YT) == 4) {
-                  *reinterpret_cast<float4*>(yp) = make_float4(v[0], v[1], v[2], v[3]);
-                } else {
-                  uint2 t;
-                  bf16* b = reinterpret_cast<bf16*>(&t);
-                  for (int e = 0; e < 4; ++e) b[e] = (bf16)v[e];
-                  *reinterpret_cast<uint2*>(yp) = t;
-                }
-              } else {
-                for (int e = 0; e < valid; ++e) yp[e] = from_f32<YT>(v[e]);
-              }
+            for (int e = 0; e < 4; ++e) {
+              float t = (acc[ms][ns][4 * g + e] + lbias_all[co + e]) * a.out_scale;
+              if (a.act == VSRK_ACT_RELU) t = fmaxf(t, 0.f);
+              if (a.has_mask) t = m[e] > 0.f ? t : 0.f;
+              if (a.has_res) t += rr[e];
+              if (a.accumulate) t += o[e];
+              v[e] = t;
+            }
+            YT* yp = reinterpret_cast<YT*>(a.y.ptr) + yoff[g];
+            if (vecs[g]) {
+              *reinterpret_cast<Pk*>(yp) = pack_pk<YT, Pk>(v);
+            } else {
+              for (int e = 0; e < valid[g]; ++e) yp[e] = from_f32<YT>(v[e]);
             }
           }
         }
@@ -238,7 +310,7 @@ __global__ __launch_bounds__(NTHR) void conv_fwd_kernel(ConvArgs a) {
   Tile cur = decode(t);
   int s = 0, buf = 0;
   issue(cur, 0, 0);
-  if (a.prologue) __syncthreads();  // lsc/lsh visible before the first commit
+  __syncthreads();  // bias / prologue tables visible
   commit(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -364,7 +436,7 @@ static int num_cus() {
   return n;
 }
 
-template <typename T, int NT, int KK, bool VEC, typename YT>
+template <typename T, int NT, int KK, int XM, typename YT>
 static int launch_fwd(ConvArgs a, hipStream_t s) {
   constexpr int MS = NT >= 128 ? 1 : 2;  // rows per wave: keeps acc + staging under 256 VGPRs
   constexpr int FTH = 8 * MS;
@@ -374,8 +446,9 @@ static int launch_fwd(ConvArgs a, hipStream_t s) {
   a.ntiles = (int)ntiles;
   if (a.ntiles == 0) return VSRK_OK;
   const int slots = (FTH + KK - 1) * (TW + KK - 1);
-  const size_t lds = (size_t)slots * ROWB + 2 * (size_t)KK * KK * NT * 64 + (a.prologue ? 2 * a.cin_pad * 4 : 0);
-  auto kern = conv_fwd_kernel<T, NT, MS, KK, VEC, YT>;
+  const size_t lds = (size_t)slots * ROWB + 2 * (size_t)KK * KK * NT * 64 + (size_t)a.cout_pad * 4 +
+                     (a.prologue ? 2 * a.cin_pad * 4 : 0);
+  auto kern = conv_fwd_kernel<T, NT, MS, KK, XM, YT>;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, NTHR, lds) != hipSuccess || per_cu < 1)
@@ -387,17 +460,27 @@ static int launch_fwd(ConvArgs a, hipStream_t s) {
   return VSRK_OK;
 }
 
-template <typename T, int KK, bool VEC, typename YT>
+template <typename T, int KK, int XM, typename YT>
 static int dispatch_nt(const ConvArgs& a, int nt, hipStream_t s) {
-  if (nt == 32) return launch_fwd<T, 32, KK, VEC, YT>(a, s);
-  if (nt == 64) return launch_fwd<T, 64, KK, VEC, YT>(a, s);
-  return launch_fwd<T, 128, KK, VEC, YT>(a, s);
+  if (nt == 32) return launch_fwd<T, 32, KK, XM, YT>(a, s);
+  if (nt == 64) return launch_fwd<T, 64, KK, XM, YT>(a, s);
+  return launch_fwd<T, 128, KK, XM, YT>(a, s);
+}
+
+template <typename T, int KK, typename YT>
+static int dispatch_xm(const ConvArgs& a, int nt, int xm, hipStream_t s) {
+  if (xm == 0) return dispatch_nt<T, KK, 0, YT>(a, nt, s);
+  if (xm == 1) return dispatch_nt<T, KK, 1, YT>(a, nt, s);
+  return dispatch_nt<T, KK, 2, YT>(a, nt, s);
 }
 
 template <typename T, typename YT>
 static int dispatch_k(const ConvArgs& a, int nt, hipStream_t s) {
-  if (a.kh == 1) return a.xvec ? dispatch_nt<T, 1, true, YT>(a, nt, s) : dispatch_nt<T, 1, false, YT>(a, nt, s);
-  return a.xvec ? dispatch_nt<T, 3, true, YT>(a, nt, s) : dispatch_nt<T, 3, false, YT>(a, nt, s);
+  // addressing mode of the input view (see conv_fwd_kernel)
+  const int64_t span = (int64_t)(8 * 2 + 2) * a.x.sh + (int64_t)(TW + 2) * a.x.sw + 64;
+  const int xm = !a.xvec ? 2 : (a.x.r > 1 || span >= (1ll << 31)) ? 1 : 0;
+  if (a.kh == 1) return dispatch_xm<T, 1, YT>(a, nt, xm, s);
+  return dispatch_xm<T, 3, YT>(a, nt, xm, s);
 }
 
 extern "C" int vsrk_conv_fwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed,

@@ -17,6 +17,8 @@ from ._native import ACT_NONE, ACT_RELU, PRO_AFFINE, PRO_AFFINE_RELU, PRO_NONE, 
 __all__ = [
     "pack_weight", "conv", "conv_wgrad", "to_view", "from_view", "relu_bwd", "add",
     "loss_fwd", "loss_bwd", "psnr", "workspace", "LOSS_KINDS",
+    "bn_stats", "bn_finalize", "bn_fold_running", "bn_relu_bwd_reduce", "bn_relu_bwd_apply",
+    "duf_dynfilter_fwd", "duf_dynfilter_bwd",
 ]
 
 LOSS_KINDS = {"L1Loss": 0, "MSELoss": 1, "HuberLoss": 2, "CharbonnierLoss": 3}
@@ -229,3 +231,93 @@ def psnr(out: torch.Tensor, target: torch.Tensor, mean: float = 0.0, std: float 
                           float(max_value),
                           ps.data_ptr(), m.data_ptr(), ws.data_ptr(), nb, N.stream_ptr(o.device)), "psnr")
     return m, ps
+
+
+# ---------------------------------------------------------------- BatchNorm --
+def _bn_ws(c: int, device) -> torch.Tensor:
+    return workspace(_lib().vsrk_bn_workspace_size(c), device)
+
+
+def bn_stats(x: torch.Tensor):
+    """Per-channel (sum, sumsq) fp32 over every voxel of a channels-last view."""
+    lib = _lib()
+    c = x.shape[-1]
+    out = torch.empty((2, c), dtype=torch.float32, device=x.device)
+    xv = N.t5(x)
+    ws = _bn_ws(c, x.device)
+    N.check(lib.vsrk_bn_stats(C.byref(xv), out[0].data_ptr(), out[1].data_ptr(), ws.data_ptr(), ws.numel(),
+                              N.stream_ptr(x.device)), "bn_stats")
+    return out
+
+
+def bn_finalize(sums: torch.Tensor, count: float, gamma, beta, eps: float, momentum: float,
+                running_mean=None, running_var=None) -> torch.Tensor:
+    """-> (4, C) fp32: scale, shift, mean, invstd (running stats updated in place)."""
+    lib = _lib()
+    c = sums.shape[1]
+    out = torch.empty((4, c), dtype=torch.float32, device=sums.device)
+    N.check(lib.vsrk_bn_finalize(sums[0].data_ptr(), sums[1].data_ptr(), float(count), N.ptr(gamma), N.ptr(beta),
+                                 float(eps), float(momentum), N.ptr(running_mean), N.ptr(running_var),
+                                 out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), out[3].data_ptr(), c,
+                                 N.stream_ptr(sums.device)), "bn_finalize")
+    return out
+
+
+def bn_fold_running(gamma, beta, running_mean, running_var, eps: float) -> torch.Tensor:
+    """eval mode -> (4, C): scale, shift (mean/invstd rows unused)."""
+    lib = _lib()
+    c = running_mean.shape[0]
+    out = torch.zeros((4, c), dtype=torch.float32, device=running_mean.device)
+    N.check(lib.vsrk_bn_fold_running(N.ptr(gamma), N.ptr(beta), running_mean.data_ptr(), running_var.data_ptr(),
+                                     float(eps), out[0].data_ptr(), out[1].data_ptr(), c,
+                                     N.stream_ptr(running_mean.device)), "bn_fold_running")
+    return out
+
+
+def bn_relu_bwd_reduce(x: torch.Tensor, dz: torch.Tensor, st: torch.Tensor) -> torch.Tensor:
+    """-> (2, C): sum_dy (= dbeta), sum_dy_xhat (= dgamma); st from bn_finalize."""
+    lib = _lib()
+    c = x.shape[-1]
+    out = torch.empty((2, c), dtype=torch.float32, device=x.device)
+    xv, gv = N.t5(x), N.t5(dz)
+    ws = _bn_ws(c, x.device)
+    N.check(lib.vsrk_bn_relu_bwd_reduce(C.byref(xv), C.byref(gv), st[0].data_ptr(), st[1].data_ptr(),
+                                        st[2].data_ptr(), st[3].data_ptr(), out[0].data_ptr(), out[1].data_ptr(),
+                                        ws.data_ptr(), ws.numel(), N.stream_ptr(x.device)), "bn_relu_bwd_reduce")
+    return out
+
+
+def bn_relu_bwd_apply(x: torch.Tensor, dz: torch.Tensor, st: torch.Tensor, gamma, red: torch.Tensor,
+                      count: float, dx: torch.Tensor, accumulate: bool = False) -> torch.Tensor:
+    lib = _lib()
+    xv, gv, ov = N.t5(x), N.t5(dz), N.t5(dx)
+    N.check(lib.vsrk_bn_relu_bwd_apply(C.byref(xv), C.byref(gv), st[0].data_ptr(), st[1].data_ptr(),
+                                       st[2].data_ptr(), st[3].data_ptr(), N.ptr(gamma), red[0].data_ptr(),
+                                       red[1].data_ptr(), float(count), C.byref(ov), 1 if accumulate else 0,
+                                       N.stream_ptr(x.device)), "bn_relu_bwd_apply")
+    return dx
+
+
+# ---------------------------------------------------------- DUF upsampling --
+def duf_dynfilter_fwd(x: torch.Tensor, logits: torch.Tensor, residual: torch.Tensor, k: int, r: int) -> torch.Tensor:
+    """x (n,h,w) fp32; logits (n,h,w,k*k*r*r) fp32; residual (n,h,w,r*r) fp32 -> (n,1,r*h,r*w) fp32."""
+    lib = _lib()
+    n, h, w = x.shape
+    out = torch.empty((n, 1, h * r, w * r), dtype=torch.float32, device=x.device)
+    N.check(lib.vsrk_duf_dynfilter_fwd(x.data_ptr(), logits.data_ptr(), residual.data_ptr(), n, h, w, k, r,
+                                       out.data_ptr(), N.stream_ptr(x.device)), "duf_dynfilter_fwd")
+    return out
+
+
+def duf_dynfilter_bwd(x: torch.Tensor, logits: torch.Tensor, gout: torch.Tensor, k: int, r: int,
+                      dtype: torch.dtype):
+    """-> (d logits (n,h,w,k*k*r*r), d residual (n,h,w,r*r)) in dtype."""
+    lib = _lib()
+    n, h, w = x.shape
+    dl = torch.empty((n, h, w, k * k * r * r), dtype=dtype, device=x.device)
+    dr = torch.empty((n, h, w, r * r), dtype=dtype, device=x.device)
+    g = gout.float().contiguous()
+    N.check(lib.vsrk_duf_dynfilter_bwd(x.data_ptr(), logits.data_ptr(), g.data_ptr(), n, h, w, k, r, dl.data_ptr(),
+                                       dr.data_ptr(), N.dtype_code(dtype), N.stream_ptr(x.device)),
+            "duf_dynfilter_bwd")
+    return dl, dr
