@@ -44,6 +44,11 @@ CASES = [
     (2, 3, 5, 33, 48, 130, (1, 1, 1), (0, 0, 0)),
     (2, 1, 11, 12, 1, 64, (1, 3, 3), (0, 1, 1)),
     (2, 1, 17, 19, 64, 1, (1, 3, 3), (0, 1, 1)),
+    # DUF heads (duf_net.py:38-49) and tail (:118) at the golden fixture's LR size
+    (2, 1, 12, 16, 256, 512, (1, 1, 1), (0, 0, 0)),
+    (2, 1, 12, 16, 512, 400, (1, 1, 1), (0, 0, 0)),
+    (2, 1, 12, 16, 256, 16, (1, 1, 1), (0, 0, 0)),
+    (2, 1, 12, 16, 256, 256, (1, 3, 3), (0, 1, 1)),
 ]
 
 

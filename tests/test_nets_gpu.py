@@ -5,24 +5,31 @@ statistics and every parameter gradient through the HIP path.
 
 Yardstick: an fp64 evaluation of the (bitwise-pinned) CPU restatement.  The
 fixture records how far the reference's own fp32 CPU path is from it
-(out_err32, ref32_err[param]); on small inputs DUF's gradients are
-ill-conditioned (BatchNorm over few voxels) and the fp32 reference itself is
-up to 1e-2 away, while EDSR's is ~1e-6.
+(out_err32, ref32_err[param]); DUF's gradients are ill-conditioned (ReLU
+masks of near-zero pre-activations flip with summation order) and the fp32
+reference itself is up to 1e-2 away, while EDSR's is ~1e-5.
 
 fp32 HIP path: output max |d| <= max(1e-4, 3*out_err32); gradient rel-L2 <=
-  max(1e-4, 3*ref32_err, 0.05*max_p ref32_err) per parameter (SURVEY §8d's
-  1e-4 wherever the reference itself is that accurate; the last term is the
-  net-wide conditioning: a parameter upstream of an ill-conditioned one sees
-  its ReLU masks / BatchNorm statistics perturbed at the same scale even when
-  the reference's own thread-count variation happens not to reach it).  The
-  BN and dynamic-filter kernels alone are checked at 1e-5..1e-4 against fp64
-  in test_bn_duf_kernels_gpu.py; parameters whose exact gradient is 0
-  (conv biases feeding a BatchNorm) |g| <= 1e-4 * max gradient norm.
+  max(1e-4, 3*ref32_err) per parameter (SURVEY §8d's 1e-4 wherever the
+  reference itself is that accurate).  ref32_err is the reference
+  algorithm's fp32 envelope: the worst of its own fp32 runs at 1/2/4/8 CPU
+  threads and of 8 fp64 runs with fp32-scale noise injected at every conv /
+  BatchNorm output and input gradient (oracle/make_golden.py).  The envelope
+  matters for DUF only: one filter-head pre-activation sits at 1.6e-7 against
+  5e-7 fp32 error, so its ReLU mask legitimately flips with summation order
+  (tools/duf_mask_flips.py), which moves filterNet.conv1.bias by 2.3e-3 and
+  everything upstream by ~3e-4.  The BN and dynamic-filter kernels alone are
+  checked at 1e-5..1e-4 against fp64 in test_bn_duf_kernels_gpu.py.
+  Parameters whose exact gradient is 0 (conv biases feeding a BatchNorm):
+  |g| <= 1e-4 * max gradient norm.
 bf16 HIP path: output max |d| <= 3e-2, mean |d| <= 3e-3; gradient rel-L2 <=
-  max(8e-2, 3*ref32_err) (0.15 for biases and BatchNorm affine parameters:
-  global sums with cancellation); zero-gradient parameters <= 2e-2 * max norm.
-  Every layer stores activations and data-gradients in bf16 (2^-9 relative
-  rounding), which over ~35 layers random-walks to the measured few %.
+  max(8e-2, 2*bf16_env) where bf16_env is the error of an *ideal*
+  bf16-storage implementation (fp64 math, bf16 weights, every conv/BN output
+  and input gradient rounded to bf16; worst of 4 dithered draws, in the
+  fixture).  Every layer stores activations and data-gradients in bf16
+  (2^-9 relative rounding), which over ~35 layers random-walks to a few % on
+  well-conditioned parameters and ~25% on DUF's BatchNorm parameters and
+  EDSR's final bias; zero-gradient parameters <= 2e-2 * max norm.
 PSNR within 0.01 dB of the reference's fp32 PSNR for both.
 """
 import pytest
@@ -95,7 +102,6 @@ def test_net_matches_golden(name, precision):
         assert (got_rs - ref.double()).abs().max().item() <= (1e-5 if precision == "fp32" else 2e-2) * (
             1 + ref.double().abs().max().item()), key
     gmax = fx["grad_max64"]
-    net_r32 = max(v for v in fx["ref32_err"].values() if v is not None)
     for k, p in net.named_parameters():
         g = p.grad.detach().cpu().double()
         r32 = fx["ref32_err"][k]
@@ -108,9 +114,8 @@ def test_net_matches_golden(name, precision):
         else:
             n64 = fx["grad_norm64"][k]
             rel = abs(g.norm().item() - n64) / n64
-        is_bn = ".bn" in k
         if precision == "fp32":
-            tol = max(1e-4, 3 * r32, 0.05 * net_r32)
+            tol = max(1e-4, 3 * r32)
         else:
-            tol = max(0.15 if (k.endswith("bias") or is_bn) else 8e-2, 3 * r32)
+            tol = max(8e-2, 2 * fx["bf16_env"][k])
         assert rel <= tol, (k, rel, tol)
