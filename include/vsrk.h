@@ -99,6 +99,11 @@ int vsrk_conv_fwd(const vsrk_conv_desc* desc, const vsrk_tensor5* x, const void*
                   const vsrk_tensor5* residual, const vsrk_tensor5* mask,
                   const vsrk_tensor5* y, void* stream);
 
+/* Tuning knob for A/B measurement: -1 (default) = bf16 fast path when
+ * eligible (env VSRK_CONV_FAST=0 disables), 0 = always the generic kernel,
+ * 1 = fast path when eligible.  Results agree within bf16 rounding. */
+int vsrk_conv_set_algo(int32_t mode);
+
 /* Weight/bias gradient (autograd of nn.Conv*d.weight/.bias in loss.backward(),
  * base_trainer.py:128).  dw is fp32 in torch layout (cout, cin, kd, kh, kw);
  * `perm_r` as in vsrk_conv_pack_weight.  Deterministic: per-workgroup fp32

@@ -186,3 +186,39 @@ def test_wgrad_prologue_and_shuffle(dtype):
     err = (dw.double().cpu() - wr.grad).abs().max().item()
     tol = (2e-5 if dtype == torch.float32 else 1e-2) * (1 + wr.grad.abs().max().item())
     assert err <= tol, err
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("combo", ["res", "mask", "mask+acc", "res+acc", "acc", "relu+mask+res+acc"])
+@pytest.mark.parametrize("shape", [(2, 1, 16, 64, 64, 64, (1, 3, 3), (0, 1, 1)),
+                                   (1, 4, 9, 40, 32, 32, (3, 3, 3), (1, 1, 1)),
+                                   (2, 1, 10, 33, 64, 96, (1, 1, 1), (0, 0, 0))])
+def test_conv_epilogue_combos(dtype, combo, shape):
+    """Every epilogue form on its own and combined (the bf16 fast path
+    specialises plain/residual/mask and routes the rest through a generic
+    copy, whose absent views alias y and must not be applied)."""
+    n, d, h, w, ci, co, k, pad = shape
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn((n, d, h, w, ci), generator=g)
+    wt = torch.randn((co, ci, *k), generator=g) / (ci * k[0] * k[1] * k[2]) ** 0.5
+    b = torch.randn(co, generator=g)
+    mask = torch.randn((n, d, h, w, co), generator=g)
+    res = torch.randn((n, d, h, w, co), generator=g)
+    y0 = torch.randn((n, d, h, w, co), generator=g)
+    parts = set(combo.split("+"))
+    ref = _ref_conv(_q(x, dtype), _q(wt, dtype), b.double(), pad) * 0.5
+    if "relu" in parts:
+        ref = torch.relu(ref)
+    if "mask" in parts:
+        ref = torch.where(_q(mask, dtype) > 0, ref, torch.zeros_like(ref))
+    if "res" in parts:
+        ref = ref + _q(res, dtype)
+    if "acc" in parts:
+        ref = ref + _q(y0, dtype)
+    yd = y0.to(DEV, dtype)
+    F.conv(x.to(DEV, dtype), F.pack_weight(wt.to(DEV), 0, dtype), yd, k, pad, bias=b.to(DEV), out_scale=0.5,
+           act=F.ACT_RELU if "relu" in parts else F.ACT_NONE,
+           mask=mask.to(DEV, dtype) if "mask" in parts else None,
+           residual=res.to(DEV, dtype) if "res" in parts else None, accumulate="acc" in parts)
+    err = (yd.double().cpu() - ref).abs().max().item()
+    assert err <= _tol(dtype, ref) * 2, err

@@ -3,6 +3,7 @@
 #pragma once
 #include "vsrk_common.h"
 #include "vsrk_internal.h"
+#include <type_traits>
 
 namespace vsrk_conv {
 
@@ -92,6 +93,30 @@ __device__ __forceinline__ void stage_prologue(float* lsc, float* lsh, int mode,
   }
 }
 
+// One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes
+// from `gsrc` land at LDS byte address lds_base + 16*l.  Written as inline asm
+// so hipcc does not track it: with the builtin, hipcc cannot tell the DMA's
+// target buffer from the one being read and drains it (s_waitcnt vmcnt(0))
+// before the first ds_read of the stage, serialising every load with the
+// MFMAs it should overlap.  The caller retires it with its own
+// `s_waitcnt vmcnt` + barrier before reading the buffer.  M0 is set and
+// restored inside the statement (hipcc reserves it).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
+}
+
 // acc += W(32 rows of co, 16-byte k slice) x X(16-byte k slice, 32 voxels)
 template <typename T>
 __device__ __forceinline__ void mma(f32x16& acc, uint4 a, uint4 b);
@@ -108,6 +133,36 @@ __device__ __forceinline__ void mma<float>(f32x16& acc, uint4 a, uint4 b) {
   acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__builtin_bit_cast(float, a.y), __builtin_bit_cast(float, b.y), acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__builtin_bit_cast(float, a.z), __builtin_bit_cast(float, b.z), acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__builtin_bit_cast(float, a.w), __builtin_bit_cast(float, b.w), acc, 0, 0, 0);
+}
+
+// 4 consecutive channels of an epilogue tensor, kept packed (uint2 for bf16,
+// uint4 for fp32) between the batched loads and the stores.
+template <typename YT, typename Pk>
+__device__ __forceinline__ Pk load_pk(const char* base, int64_t off, bool vec, int valid) {
+  const YT* p = reinterpret_cast<const YT*>(base) + off;
+  if (vec) return *reinterpret_cast<const Pk*>(p);
+  Pk v;
+  YT* q = reinterpret_cast<YT*>(&v);
+  for (int e = 0; e < 4; ++e) q[e] = e < valid ? p[e] : from_f32<YT>(0.f);
+  return v;
+}
+template <typename YT, typename Pk>
+__device__ __forceinline__ void unpack_pk(Pk v, float* f) {
+  const YT* q = reinterpret_cast<const YT*>(&v);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) f[e] = to_f32<YT>(q[e]);
+}
+template <typename YT>
+__device__ __forceinline__ void unpack_pk(uint2 v, float* f) { unpack_pk<YT, uint2>(v, f); }
+template <typename YT>
+__device__ __forceinline__ void unpack_pk(uint4 v, float* f) { unpack_pk<YT, uint4>(v, f); }
+template <typename YT, typename Pk>
+__device__ __forceinline__ Pk pack_pk(const float* f) {
+  Pk v;
+  YT* q = reinterpret_cast<YT*>(&v);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) q[e] = from_f32<YT>(f[e]);
+  return v;
 }
 
 template <typename YT>

@@ -22,36 +22,6 @@
 namespace {
 using namespace vsrk_conv;
 
-// 4 consecutive channels of an epilogue tensor, kept packed (uint2 for bf16,
-// uint4 for fp32) between the batched loads and the stores.
-template <typename YT, typename Pk>
-__device__ __forceinline__ Pk load_pk(const char* base, int64_t off, bool vec, int valid) {
-  const YT* p = reinterpret_cast<const YT*>(base) + off;
-  if (vec) return *reinterpret_cast<const Pk*>(p);
-  Pk v;
-  YT* q = reinterpret_cast<YT*>(&v);
-  for (int e = 0; e < 4; ++e) q[e] = e < valid ? p[e] : from_f32<YT>(0.f);
-  return v;
-}
-template <typename YT, typename Pk>
-__device__ __forceinline__ void unpack_pk(Pk v, float* f) {
-  const YT* q = reinterpret_cast<const YT*>(&v);
-#pragma unroll
-  for (int e = 0; e < 4; ++e) f[e] = to_f32<YT>(q[e]);
-}
-template <typename YT>
-__device__ __forceinline__ void unpack_pk(uint2 v, float* f) { unpack_pk<YT, uint2>(v, f); }
-template <typename YT>
-__device__ __forceinline__ void unpack_pk(uint4 v, float* f) { unpack_pk<YT, uint4>(v, f); }
-template <typename YT, typename Pk>
-__device__ __forceinline__ Pk pack_pk(const float* f) {
-  Pk v;
-  YT* q = reinterpret_cast<YT*>(&v);
-#pragma unroll
-  for (int e = 0; e < 4; ++e) q[e] = from_f32<YT>(f[e]);
-  return v;
-}
-
 // ---------------------------------------------------------------------------
 // forward / data-gradient
 // ---------------------------------------------------------------------------
@@ -212,9 +182,7 @@ __global__ __launch_bounds__(NTHR) void conv_fwd_kernel(ConvArgs a) {
 #pragma unroll
     for (int jj = 0; jj < NBJ; ++jj) {
       const int gi = wave + 8 * jj;
-      if (gi < NBI)
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(wb + b_rel[jj]),
-                                         (void __attribute__((address_space(3)))*)(bdst + gi * 1024), 16, 0, 0);
+      if (gi < NBI) glds16(wb + b_rel[jj], __builtin_amdgcn_readfirstlane(lds_addr(bdst + gi * 1024)));
     }
   };
   auto commit = [&](int s) __attribute__((always_inline)) {
@@ -537,6 +505,8 @@ extern "C" int vsrk_conv_fwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, con
   const int NT = y->c <= 32 ? 32 : ((y->c <= 64 || d->kh == 3) ? 64 : 128);
   a.ntn = ceil_div(y->c, NT);
   hipStream_t s = (hipStream_t)stream;
+  const int fast = vsrk_conv_fwd_fast(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s);
+  if (fast != 0) return fast > 0 ? VSRK_OK : -fast;
   if (xdt == VSRK_BF16) {
     if (ydt == VSRK_BF16) return dispatch_k<bf16, bf16>(a, NT, s);
     return dispatch_k<bf16, float>(a, NT, s);

@@ -9,3 +9,9 @@
 size_t vsrk_channel_reduce_ws_bytes(int c);
 int vsrk_channel_reduce_internal(const vsrk_tensor5* x, int mode, int perm_r, float scale, float* sum,
                                  float* sumsq, int accumulate, void* ws, size_t ws_bytes, hipStream_t s);
+
+// bf16 fast path of vsrk_conv_fwd (conv_fast.hip): 1 = launched, 0 = not
+// eligible (use the generic kernel), < 0 = -(error status).
+int vsrk_conv_fwd_fast(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                       const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
+                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
