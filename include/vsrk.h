@@ -40,7 +40,7 @@ enum {
 enum { VSRK_F32 = 0, VSRK_BF16 = 1 };
 
 enum { VSRK_PRO_NONE = 0, VSRK_PRO_RELU = 1, VSRK_PRO_AFFINE = 2, VSRK_PRO_AFFINE_RELU = 3 };
-enum { VSRK_ACT_NONE = 0, VSRK_ACT_RELU = 1 };
+enum { VSRK_ACT_NONE = 0, VSRK_ACT_RELU = 1, VSRK_ACT_PRELU = 2 };
 
 /* Channels-last view.  Element (n,d,h,w,c) lives at
  *   ptr + n*sn + d*sd + h*sh + w*sw + c                      (shuffle <= 1)
@@ -73,6 +73,9 @@ typedef struct vsrk_conv_desc {
   float out_scale;    /* multiplies (acc + bias) — EDSR res_scale (edsr_net.py:51) */
   int32_t accumulate; /* 1: out += result (gradient accumulation into concat buffers) */
   int32_t bias_perm_r; /* >1: bias is in torch pixel-shuffle order (see vsrk_conv_pack_weight perm_r) */
+  const float* act_param;  /* device scalar, VSRK_ACT_PRELU: nn.PReLU(num_parameters=1) slope (drf_net.py:56) */
+  const float* mask_slope; /* device scalar or NULL: where mask <= 0 the output is scaled by *mask_slope
+                              instead of zeroed -- the PReLU backward dx = dy * (y > 0 ? 1 : a) */
 } vsrk_conv_desc;
 
 /* Repack an fp32 torch conv weight (cout, cin, kd, kh, kw) into the kernel
@@ -115,6 +118,43 @@ int vsrk_conv_wgrad(const vsrk_conv_desc* desc, const vsrk_tensor5* x, const vsr
                     const float* pro_scale, const float* pro_shift, float dy_scale, int32_t perm_r,
                     float* dw, float* dbias, int32_t accumulate, void* workspace,
                     size_t workspace_bytes, void* stream);
+
+/* Strided up/down projections of DRF's feedback block (drf_net.py:70-102):
+ * nn.Conv2d(cin, cout, k, stride s, padding p) and nn.ConvTranspose2d(cin,
+ * cout, k, s, p) with k <= p + 2s, p <= s (DRF: (6,2,2) (7,3,2) (8,4,2)
+ * (12,8,2)) are exactly 3x3 / pad-1 convolutions on the sub-pixel grid:
+ *  - the strided conv reads its high-res input through a shuffle-s view
+ *    (s*s*cin logical channels) and is a plain 3x3 conv cin' = s*s*cin -> cout;
+ *  - the transposed conv is a 3x3 conv cin -> s*s*cout written through a
+ *    shuffle-s output view.
+ * vsrk_subpixel_conv_weight builds that equivalent fp32 weight (torch layout,
+ * view channel order; tap/sub-pixel pairs outside the k x k kernel are zero)
+ * and bias; vsrk_subpixel_wgrad_fold maps the equivalent conv's weight/bias
+ * gradient back onto the k x k weight (each entry has exactly one image) and
+ * sums the transposed conv's bias gradient over sub-pixels in a fixed order.
+ * transposed = 0: w (cout, cin, k, k) -> weq (cout, s*s*cin, 3, 3), beq (cout)
+ * transposed = 1: w (cin, cout, k, k) -> weq (s*s*cout, cin, 3, 3), beq (s*s*cout) */
+int vsrk_subpixel_conv_weight(const float* w, const float* bias, int32_t cin, int32_t cout, int32_t k, int32_t s,
+                              int32_t p, int32_t transposed, float* weq, float* beq, void* stream);
+int vsrk_subpixel_wgrad_fold(const float* dweq, const float* dbeq, int32_t cin, int32_t cout, int32_t k, int32_t s,
+                             int32_t p, int32_t transposed, float* dw, float* db, int32_t accumulate, void* stream);
+
+/* nn.PReLU(num_parameters=1) weight gradient (drf_net.py:56-102), from the
+ * layer's output y and the gradient dx at its input (as the conv epilogues
+ * produce it, dx = dy * (y > 0 ? 1 : a)):  da = sum_{y < 0} dx * y / a^2
+ * (= sum_{x < 0} dy * x).  Deterministic two-pass reduction; *da is written
+ * (accumulate = 0) or added to.  Workspace: vsrk_prelu_workspace_size(). */
+size_t vsrk_prelu_workspace_size(void);
+int vsrk_prelu_wgrad(const vsrk_tensor5* y, const vsrk_tensor5* dx, const float* a, float* da, int32_t accumulate,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* nn.PReLU backward in one pass: dx = (dy [+ dy2]) * (y > 0 ? 1 : a) for the
+ * layer output y (dy2 may be NULL: a second gradient contribution, e.g. a
+ * skip connection), and da [+]= sum_{y<0} dx * y / a^2.  dx may alias dy.
+ * Workspace: vsrk_prelu_workspace_size(). */
+int vsrk_prelu_bwd(const vsrk_tensor5* y, const vsrk_tensor5* dy, const vsrk_tensor5* dy2, const float* a,
+                   const vsrk_tensor5* dx, float* da, int32_t accumulate_da, void* workspace, size_t workspace_bytes,
+                   void* stream);
 
 /* Layout/dtype moves between torch's NC(D)HW fp32 tensors and channels-last
  * views: src is (n, c, d, h, w) fp32 contiguous; channels beyond c in dst are

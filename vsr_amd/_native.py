@@ -17,7 +17,7 @@ from . import build as _build
 VSRK_F32 = 0
 VSRK_BF16 = 1
 PRO_NONE, PRO_RELU, PRO_AFFINE, PRO_AFFINE_RELU = 0, 1, 2, 3
-ACT_NONE, ACT_RELU = 0, 1
+ACT_NONE, ACT_RELU, ACT_PRELU = 0, 1, 2
 
 _DTYPE = {torch.float32: VSRK_F32, torch.bfloat16: VSRK_BF16}
 
@@ -41,6 +41,8 @@ class ConvDesc(C.Structure):
         ("out_scale", C.c_float),
         ("accumulate", C.c_int32),
         ("bias_perm_r", C.c_int32),
+        ("act_param", C.c_void_p),
+        ("mask_slope", C.c_void_p),
     ]
 
 
@@ -74,6 +76,12 @@ _SIGS = {
     "vsrk_bn_relu_bwd_apply": (C.c_int, [_T5, _T5, _P, _P, _P, _P, _P, _P, _P, C.c_double, _T5, C.c_int32, _P]),
     "vsrk_duf_dynfilter_fwd": (C.c_int, [_P, _P, _P] + [C.c_int32] * 5 + [_P, _P]),
     "vsrk_duf_dynfilter_bwd": (C.c_int, [_P, _P, _P] + [C.c_int32] * 5 + [_P, _P, C.c_int32, _P]),
+    "vsrk_conv_set_algo": (C.c_int, [C.c_int32]),
+    "vsrk_subpixel_conv_weight": (C.c_int, [_P, _P] + [C.c_int32] * 6 + [_P, _P, _P]),
+    "vsrk_subpixel_wgrad_fold": (C.c_int, [_P, _P] + [C.c_int32] * 6 + [_P, _P, C.c_int32, _P]),
+    "vsrk_prelu_workspace_size": (C.c_size_t, []),
+    "vsrk_prelu_wgrad": (C.c_int, [_T5, _T5, _P, _P, C.c_int32, _P, C.c_size_t, _P]),
+    "vsrk_prelu_bwd": (C.c_int, [_T5, _T5, _T5, _P, _T5, _P, C.c_int32, _P, C.c_size_t, _P]),
     "vsrk_last_error": (C.c_char_p, []),
     "vsrk_version": (C.c_char_p, []),
 }

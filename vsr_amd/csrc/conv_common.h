@@ -35,6 +35,8 @@ struct ConvArgs {
   int kd, kh, kw, pd, ph, pw;
   int prologue, act, accumulate, has_res, has_mask, xvec, bias_r;
   float out_scale;
+  const float* act_param;   // PReLU slope (device scalar)
+  const float* mask_slope;  // masked-off scale (device scalar) or null (0)
   int tiles_h, tiles_w, ntn, nblk;
   int ntiles;  // output tiles (incl. N tiles) walked by the persistent grid
 };
@@ -115,6 +117,16 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
 }
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
+}
+
+// Epilogue activation / mask helpers shared by the conv kernels.
+__device__ __forceinline__ float act_apply(int act, float t, float slope) {
+  if (act == VSRK_ACT_RELU) return fmaxf(t, 0.f);
+  if (act == VSRK_ACT_PRELU) return t > 0.f ? t : slope * t;
+  return t;
+}
+__device__ __forceinline__ float mask_apply(float m, float t, float mslope) {
+  return m > 0.f ? t : (mslope != 0.f ? mslope * t : 0.f);
 }
 
 // acc += W(32 rows of co, 16-byte k slice) x X(16-byte k slice, 32 voxels)

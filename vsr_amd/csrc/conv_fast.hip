@@ -48,6 +48,8 @@ struct FastArgs {
   int kd, pd, ph, pw;
   int prologue, act, accumulate, has_res, has_mask, bias_r;
   float out_scale;
+  const float* act_param;
+  const float* mask_slope;
   int tiles_h, tiles_w, ntn, ntiles;
   int ablate;  // diagnostics only (VSRK_FAST_ABLATE): 1 skip DMA after the first stage, 2 skip MFMAs, 4 skip epilogue
 };
@@ -79,6 +81,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: SALU address math
   float* lbias = reinterpret_cast<float*>(lds + 2 * SLOT + (SCR_OWN ? NW * 32 * (CB * 4 + 16) : 0));  // [cout_pad], view order
+  const float aslope = a.act == VSRK_ACT_PRELU ? *a.act_param : 0.f;
+  const float mslope = a.mask_slope ? *a.mask_slope : 0.f;
   auto SCR_BASE = [&](int sl) __attribute__((always_inline)) { return SCR_OWN ? 2 * SLOT : sl * SLOT; };
   int slot_epi = 0;  // the ring slot free during the deferred epilogue
   float* lsc = lbias + a.cout_pad;
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
                use_acc = (MODE & 4) && a.accumulate;
     using Pk = typename std::conditional<sizeof(YT) == 4, uint4, uint2>::type;
     const bool full = tl.h0 + FTH <= a.y.h && tl.w0 + TW <= a.y.w && tl.n0 + NT <= a.cout;
-    const bool relu = a.act == VSRK_ACT_RELU;
+    const bool act = a.act != VSRK_ACT_NONE;
     const float osc = a.out_scale;
 #pragma unroll
     for (int ms = 0; ms < MS; ++ms) {
@@ -359,15 +363,15 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
           const float4 bs = *reinterpret_cast<const float4*>(lbias + co);
           float v[4] = {fmaf(acc[ms][ns][4 * g + 0], osc, bs.x), fmaf(acc[ms][ns][4 * g + 1], osc, bs.y),
                         fmaf(acc[ms][ns][4 * g + 2], osc, bs.z), fmaf(acc[ms][ns][4 * g + 3], osc, bs.w)};
-          if (relu) {
+          if (act) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+            for (int e = 0; e < 4; ++e) v[e] = act_apply(a.act, v[e], aslope);
           }
           if ((MODE & 2) && use_msk) {
             float mm[4];
             unpack_pk<YT>(mv[g], mm);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = mm[e] > 0.f ? v[e] : 0.f;
+            for (int e = 0; e < 4; ++e) v[e] = mask_apply(mm[e], v[e], mslope);
           }
           if constexpr (MODE & 1) {
             float rr[4];
@@ -416,7 +420,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
     constexpr int VPI = 64 / LPV;  // voxels per wave instruction
     constexpr int RS = CB * 4 + 16;
     char* scr = lds + SCR_BASE(slot_epi) + wave * 32 * RS;
-    const bool relu = a.act == VSRK_ACT_RELU;
+    const bool act = a.act != VSRK_ACT_NONE;
     const float osc = a.out_scale;
     const int c8 = (lane % LPV) * 8;
 #pragma unroll
@@ -458,7 +462,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             t[e] = fmaf(t[e], osc, bsv[e]);
-            if (relu) t[e] = fmaxf(t[e], 0.f);
+            if (act) t[e] = act_apply(a.act, t[e], aslope);
           }
           bf16* yp = reinterpret_cast<bf16*>(a.y.ptr) + yrow + (int64_t)wo * yr * a.y.sw;
           if ((MODE & 2) && use_msk) {
@@ -468,7 +472,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
             float m[8];
             Chunk<bf16>::unpack(mv, m);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) t[e] = m[e] > 0.f ? t[e] : 0.f;
+            for (int e = 0; e < 8; ++e) t[e] = mask_apply(m[e], t[e], mslope);
           }
           if ((MODE & 1) && use_res) {
             const bf16* rp = reinterpret_cast<const bf16*>(a.res.ptr) + (tl.nb * a.res.sn + (int64_t)tl.dz * a.res.sd +
@@ -578,6 +582,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
 }
 
 int g_fast_mode = -1;  // -1: from VSRK_CONV_FAST (default on), 0 off, 1 on
+constexpr int kNotEligible = -1000;
 
 int num_cus_fast() {
   static int n = 0;
@@ -605,7 +610,7 @@ int launch_fast(FastArgs a, hipStream_t s) {
   if (a.ntiles == 0) return VSRK_OK;
   const size_t lds = 2 * (size_t)SLOT + (SCR_OWN ? NW * 32 * (CB * 4 + 16) : 0) + (size_t)a.cout_pad * 4 +
                      (PRO ? 2 * (size_t)a.cin_pad * 4 : 0);
-  VSRK_CHECK(lds <= 160 * 1024, "conv_fwd: fast-path LDS %zu too large", lds);
+  if (lds > 160 * 1024) return kNotEligible;  // e.g. a 4096-entry bias table: generic kernel
   auto kern = conv_fast_kernel<KK, NT, MS, XS, YS, PRO, YT, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int grid = (int)std::min<int64_t>(ntiles, (int64_t)num_cus_fast());
@@ -682,6 +687,8 @@ int vsrk_conv_fwd_fast(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   a.has_mask = mask != nullptr;
   a.bias_r = d->bias_perm_r;
   a.out_scale = d->out_scale;
+  a.act_param = d->act_param;
+  a.mask_slope = d->mask_slope;
   a.tiles_w = ceil_div(y->w, TW);
   const int NT = y->c <= 32 ? 32 : (y->c <= 64 || d->kh == 3) ? 64 : 128;
   a.ntn = ceil_div(y->c, NT);
@@ -716,5 +723,6 @@ int vsrk_conv_fwd_fast(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   }
 #undef VSRK_FAST_Y
 #undef VSRK_FAST_Y3
+  if (rc == kNotEligible) return 0;
   return rc == VSRK_OK ? 1 : -rc;
 }

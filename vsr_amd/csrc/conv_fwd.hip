@@ -62,6 +62,8 @@ __global__ __launch_bounds__(NTHR) void conv_fwd_kernel(ConvArgs a) {
   float* lsc = lbias_all + a.cout_pad;
   float* lsh = lsc + a.cin_pad;
   const bool relu_in = (a.prologue & VSRK_PRO_RELU) != 0;
+  const float aslope = a.act == VSRK_ACT_PRELU ? *a.act_param : 0.f;
+  const float mslope = a.mask_slope ? *a.mask_slope : 0.f;
   if (a.prologue) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, a.cin_pad, tid, NTHR);
   for (int i = tid; i < a.cout_pad; i += NTHR) {
     float b = 0.f;
@@ -249,8 +251,8 @@ __global__ __launch_bounds__(NTHR) void conv_fwd_kernel(ConvArgs a) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               float t = (acc[ms][ns][4 * g + e] + lbias_all[co + e]) * a.out_scale;
-              if (a.act == VSRK_ACT_RELU) t = fmaxf(t, 0.f);
-              if (a.has_mask) t = m[e] > 0.f ? t : 0.f;
+              t = act_apply(a.act, t, aslope);
+              if (a.has_mask) t = mask_apply(m[e], t, mslope);
               if (a.has_res) t += rr[e];
               if (a.accumulate) t += o[e];
               v[e] = t;
@@ -466,6 +468,8 @@ extern "C" int vsrk_conv_fwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, con
   VSRK_CHECK(x->n == y->n, "conv_fwd: batch mismatch");
   VSRK_CHECK(x->h < 32768 && x->w < 32768, "conv_fwd: spatial size too large");
   VSRK_CHECK(!(d->prologue & VSRK_PRO_AFFINE) || (pro_scale && pro_shift), "conv_fwd: affine prologue needs scale/shift");
+  VSRK_CHECK(d->act != VSRK_ACT_PRELU || d->act_param, "conv_fwd: PReLU activation needs act_param");
+  VSRK_CHECK(d->act >= VSRK_ACT_NONE && d->act <= VSRK_ACT_PRELU, "conv_fwd: bad act %d", d->act);
   const int yr = y->shuffle > 1 ? y->shuffle : 1;
   VSRK_CHECK(yr == 1 || (y->c / (yr * yr)) % 4 == 0, "conv_fwd: shuffled output needs c/r^2 %% 4 == 0");
   if (residual) {
@@ -499,6 +503,8 @@ extern "C" int vsrk_conv_fwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, con
   a.xvec = chunk_ok(x, es);
   a.bias_r = d->bias_perm_r;
   a.out_scale = d->out_scale;
+  a.act_param = d->act_param;
+  a.mask_slope = d->mask_slope;
   a.tiles_w = ceil_div(y->w, TW);
   // NT=128 only for 1x1 kernels (a double-buffered 3x3 weight slice of 128
   // channels would not fit LDS); wider 3x3 outputs use several 64-wide tiles

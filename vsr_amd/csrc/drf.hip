@@ -1,0 +1,281 @@
+// Kernels specific to the DRF feedback generator (drf_net.py:8-147).
+//
+//  * Sub-pixel weight transforms: the feedback block's strided projections
+//    nn.Conv2d(k, stride s, pad p) / nn.ConvTranspose2d(k, s, p)
+//    (drf_net.py:70-102) become 3x3 pad-1 convolutions on the low-res grid
+//    (see include/vsrk.h), so they run on the implicit-GEMM MFMA kernels with
+//    a shuffle-s input view (strided conv) or output view (transposed conv).
+//    For an output sub-pixel offset i in [0, s) and conv tap kh in {0,1,2}
+//    (input row offset kh - 1):
+//        strided conv:    kernel row s*(kh - 1) + i + p
+//        transposed conv: kernel row s*(1 - kh) + i + p
+//    (zero when outside [0, k)); every kernel entry has exactly one image.
+//  * PReLU slope gradient: da = sum_{y<0} dx * y / a^2 over a channels-last
+//    view, two-pass fixed-order reduction (deterministic).
+#include "vsrk_common.h"
+#include "vsrk_internal.h"
+
+namespace {
+
+__device__ __forceinline__ int sp_row(int transposed, int s, int p, int tap, int sub) {
+  return transposed ? s * (1 - tap) + sub + p : s * (tap - 1) + sub + p;
+}
+
+// one thread per equivalent-weight element (torch layout (co', ci', 3, 3))
+__global__ void subpixel_weight_kernel(const float* __restrict__ w, const float* __restrict__ bias, int cin,
+                                       int cout, int k, int s, int p, int transposed, float* __restrict__ weq,
+                                       float* __restrict__ beq, int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int kw = idx % 3, kh = (idx / 3) % 3;
+  const int64_t t = idx / 9;
+  const int cip = transposed ? cin : s * s * cin;  // equivalent input channels
+  const int ci_e = t % cip, co_e = t / cip;
+  int co, ci, sub;
+  if (transposed) {
+    sub = co_e / cout;
+    co = co_e - sub * cout;
+    ci = ci_e;
+  } else {
+    sub = ci_e / cin;
+    ci = ci_e - sub * cin;
+    co = co_e;
+  }
+  const int si = sub / s, sj = sub - si * s;
+  const int ky = sp_row(transposed, s, p, kh, si), kx = sp_row(transposed, s, p, kw, sj);
+  float v = 0.f;
+  if (ky >= 0 && ky < k && kx >= 0 && kx < k) {
+    const int64_t widx = transposed ? (((int64_t)ci * cout + co) * k + ky) * k + kx
+                                    : (((int64_t)co * cin + ci) * k + ky) * k + kx;
+    v = w[widx];
+  }
+  weq[idx] = v;
+  if (beq && kh == 0 && kw == 0 && ci_e == 0) beq[co_e] = bias ? bias[co] : 0.f;
+}
+
+// one thread per k x k weight element: gather its single equivalent entry
+__global__ void subpixel_fold_kernel(const float* __restrict__ dweq, const float* __restrict__ dbeq, int cin,
+                                     int cout, int k, int s, int p, int transposed, float* __restrict__ dw,
+                                     float* __restrict__ db, int accumulate, int64_t total) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < total) {
+    const int kx = idx % k, ky = (idx / k) % k;
+    const int64_t t = idx / (k * k);
+    // transposed: idx over (cin, cout, k, k); else (cout, cin, k, k)
+    const int b = t % (transposed ? cout : cin), a = t / (transposed ? cout : cin);
+    const int ci = transposed ? a : b, co = transposed ? b : a;
+    // solve ky = s*(+-(kh-1)) + si + p for (kh, si) with kh in {0,1,2}, si in [0, s)
+    int kh = -1, si = 0, kw = -1, sj = 0;
+    for (int q = 0; q < 3; ++q) {
+      const int ry = ky - sp_row(transposed, s, p, q, 0);
+      if (ry >= 0 && ry < s) { kh = q; si = ry; }
+      const int rx = kx - sp_row(transposed, s, p, q, 0);
+      if (rx >= 0 && rx < s) { kw = q; sj = rx; }
+    }
+    float v = 0.f;
+    if (kh >= 0 && kw >= 0) {
+      const int sub = si * s + sj;
+      const int co_e = transposed ? sub * cout + co : co;
+      const int ci_e = transposed ? ci : sub * cin + ci;
+      const int cip = transposed ? cin : s * s * cin;
+      v = dweq[(((int64_t)co_e * cip + ci_e) * 3 + kh) * 3 + kw];
+    }
+    dw[idx] = accumulate ? dw[idx] + v : v;
+  }
+  if (db && idx < cout) {
+    float v = 0.f;
+    if (transposed) {
+      for (int sub = 0; sub < s * s; ++sub) v += dbeq[sub * cout + idx];  // fixed order
+    } else {
+      v = dbeq[idx];
+    }
+    db[idx] = accumulate ? db[idx] + v : v;
+  }
+}
+
+constexpr int PRELU_BLOCKS = 512;
+
+template <typename T>
+__global__ __launch_bounds__(256) void prelu_partial_kernel(View y, View dx, int64_t nvox, double* __restrict__ part) {
+  // each thread walks 8-channel chunks of voxels: (voxel, chunk) flattened
+  constexpr int E = 16 / sizeof(T);
+  const int cpv = (y.c + E - 1) / E;
+  const int64_t total = nvox * cpv;
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % cpv) * E;
+    int64_t v = i / cpv;
+    const int w = v % y.w; v /= y.w;
+    const int h = v % y.h; v /= y.h;
+    const int d = v % y.d;
+    const int n = v / y.d;
+    const T* py = reinterpret_cast<const T*>(y.ptr) + view_off(y, n, d, h, w, ch);
+    const T* pd = reinterpret_cast<const T*>(dx.ptr) + view_off(dx, n, d, h, w, ch);
+    float acc = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (ch + e < y.c) {
+        const float yv = to_f32<T>(py[e]);
+        if (yv < 0.f) acc = fmaf(to_f32<T>(pd[e]), yv, acc);
+      }
+    }
+    s += acc;
+  }
+  __shared__ double sh[256];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) sh[threadIdx.x] += sh[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = sh[0];
+}
+
+__global__ void prelu_final_kernel(const double* __restrict__ part, int nblk, const float* __restrict__ a,
+                                   float* __restrict__ da, int accumulate) {
+  __shared__ double sh[256];
+  double s = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x) s += part[b];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) sh[threadIdx.x] += sh[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double av = (double)*a;
+    const float v = (float)(sh[0] / (av * av));
+    *da = accumulate ? *da + v : v;
+  }
+}
+
+}  // namespace
+
+extern "C" int vsrk_subpixel_conv_weight(const float* w, const float* bias, int32_t cin, int32_t cout, int32_t k,
+                                         int32_t s, int32_t p, int32_t transposed, float* weq, float* beq,
+                                         void* stream) {
+  VSRK_CHECK(w && weq, "subpixel_conv_weight: null pointer");
+  VSRK_CHECK(s >= 1 && p >= 0 && p <= s && k <= p + 2 * s && k >= 1,
+             "subpixel_conv_weight: (k=%d, s=%d, p=%d) is not a 3x3 sub-pixel conv (needs p <= s, k <= p + 2s)", k, s,
+             p);
+  const int cop = transposed ? s * s * cout : cout, cip = transposed ? cin : s * s * cin;
+  const int64_t total = (int64_t)cop * cip * 9;
+  subpixel_weight_kernel<<<(int)ceil_div64(total, 256), 256, 0, (hipStream_t)stream>>>(w, bias, cin, cout, k, s, p,
+                                                                                       transposed, weq, beq, total);
+  VSRK_LAUNCH_CHECK("subpixel_conv_weight");
+  return VSRK_OK;
+}
+
+extern "C" int vsrk_subpixel_wgrad_fold(const float* dweq, const float* dbeq, int32_t cin, int32_t cout, int32_t k,
+                                        int32_t s, int32_t p, int32_t transposed, float* dw, float* db,
+                                        int32_t accumulate, void* stream) {
+  VSRK_CHECK(dweq && dw, "subpixel_wgrad_fold: null pointer");
+  VSRK_CHECK(!db || dbeq, "subpixel_wgrad_fold: dbias needs the equivalent dbias");
+  VSRK_CHECK(s >= 1 && p >= 0 && p <= s && k <= p + 2 * s && k >= 1, "subpixel_wgrad_fold: bad (k, s, p)");
+  const int64_t total = (int64_t)cin * cout * k * k;
+  const int64_t n = std::max<int64_t>(total, db ? cout : 0);
+  subpixel_fold_kernel<<<(int)ceil_div64(n, 256), 256, 0, (hipStream_t)stream>>>(dweq, dbeq, cin, cout, k, s, p,
+                                                                                transposed, dw, db, accumulate, total);
+  VSRK_LAUNCH_CHECK("subpixel_wgrad_fold");
+  return VSRK_OK;
+}
+
+extern "C" size_t vsrk_prelu_workspace_size(void) { return PRELU_BLOCKS * sizeof(double); }
+
+extern "C" int vsrk_prelu_wgrad(const vsrk_tensor5* y, const vsrk_tensor5* dx, const float* a, float* da,
+                                int32_t accumulate, void* workspace, size_t workspace_bytes, void* stream) {
+  VSRK_CHECK(y && dx && y->ptr && dx->ptr && a && da, "prelu_wgrad: null argument");
+  VSRK_CHECK(y->dtype == dx->dtype, "prelu_wgrad: dtype mismatch");
+  VSRK_CHECK(y->n == dx->n && y->d == dx->d && y->h == dx->h && y->w == dx->w && y->c == dx->c,
+             "prelu_wgrad: shape mismatch");
+  VSRK_CHECK(y->shuffle <= 1 && dx->shuffle <= 1, "prelu_wgrad: plain views only");
+  VSRK_CHECK(workspace && workspace_bytes >= vsrk_prelu_workspace_size(), "prelu_wgrad: workspace too small");
+  const View vy = make_view(y), vd = make_view(dx);
+  const int64_t nvox = (int64_t)y->n * y->d * y->h * y->w;
+  hipStream_t s = (hipStream_t)stream;
+  double* part = (double*)workspace;
+  if (y->dtype == VSRK_BF16)
+    prelu_partial_kernel<bf16><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vd, nvox, part);
+  else
+    prelu_partial_kernel<float><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vd, nvox, part);
+  VSRK_LAUNCH_CHECK("prelu_partial");
+  prelu_final_kernel<<<1, 256, 0, s>>>(part, PRELU_BLOCKS, a, da, accumulate);
+  VSRK_LAUNCH_CHECK("prelu_final");
+  return VSRK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// PReLU backward (drf_net.py:56-106): dx = (dy [+ dy2]) * (y > 0 ? 1 : a) and,
+// in the same pass, da = sum_{y<0} dx * y / a^2, as per-block partials
+// reduced in a fixed order.
+namespace {
+template <typename T>
+__global__ __launch_bounds__(256) void prelu_bwd_kernel(View y, View dy, View dy2, int has2, const float* __restrict__ a,
+                                                        View dx, int64_t nvox, double* __restrict__ part) {
+  constexpr int E = 16 / sizeof(T);
+  const int cpv = (y.c + E - 1) / E;
+  const int64_t total = nvox * cpv;
+  const float av = *a;
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % cpv) * E;
+    int64_t v = i / cpv;
+    const int w = v % y.w; v /= y.w;
+    const int h = v % y.h; v /= y.h;
+    const int d = v % y.d;
+    const int n = v / y.d;
+    const T* py = reinterpret_cast<const T*>(y.ptr) + view_off(y, n, d, h, w, ch);
+    const T* pg = reinterpret_cast<const T*>(dy.ptr) + view_off(dy, n, d, h, w, ch);
+    const T* pg2 = has2 ? reinterpret_cast<const T*>(dy2.ptr) + view_off(dy2, n, d, h, w, ch) : nullptr;
+    T* po = reinterpret_cast<T*>(dx.ptr) + view_off(dx, n, d, h, w, ch);
+    float acc = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (ch + e < y.c) {
+        const float yv = to_f32<T>(py[e]);
+        float g = to_f32<T>(pg[e]);
+        if (has2) g += to_f32<T>(pg2[e]);
+        const T o = from_f32<T>(yv > 0.f ? g : av * g);
+        po[e] = o;
+        if (yv < 0.f) acc = fmaf(to_f32<T>(o), yv, acc);
+      }
+    }
+    s += acc;
+  }
+  __shared__ double sh[256];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) sh[threadIdx.x] += sh[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = sh[0];
+}
+}  // namespace
+
+extern "C" int vsrk_prelu_bwd(const vsrk_tensor5* y, const vsrk_tensor5* dy, const vsrk_tensor5* dy2, const float* a,
+                              const vsrk_tensor5* dx, float* da, int32_t accumulate_da, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  VSRK_CHECK(y && dy && dx && a && da && y->ptr && dy->ptr && dx->ptr, "prelu_bwd: null argument");
+  for (const vsrk_tensor5* t : {dy, dy2, dx}) {
+    if (!t) continue;
+    VSRK_CHECK(t->dtype == y->dtype && t->n == y->n && t->d == y->d && t->h == y->h && t->w == y->w &&
+                   t->c == y->c && t->shuffle <= 1,
+               "prelu_bwd: view mismatch");
+  }
+  VSRK_CHECK(y->shuffle <= 1, "prelu_bwd: plain views only");
+  VSRK_CHECK(workspace && workspace_bytes >= vsrk_prelu_workspace_size(), "prelu_bwd: workspace too small");
+  const View vy = make_view(y), vg = make_view(dy), vo = make_view(dx);
+  const View vg2 = dy2 ? make_view(dy2) : vg;
+  const int64_t nvox = (int64_t)y->n * y->d * y->h * y->w;
+  hipStream_t s = (hipStream_t)stream;
+  double* part = (double*)workspace;
+  if (y->dtype == VSRK_BF16)
+    prelu_bwd_kernel<bf16><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, nvox, part);
+  else
+    prelu_bwd_kernel<float><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, nvox, part);
+  VSRK_LAUNCH_CHECK("prelu_bwd");
+  prelu_final_kernel<<<1, 256, 0, s>>>(part, PRELU_BLOCKS, a, da, accumulate_da);
+  VSRK_LAUNCH_CHECK("prelu_final");
+  return VSRK_OK;
+}

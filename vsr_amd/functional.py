@@ -12,13 +12,14 @@ import ctypes as C
 import torch
 
 from . import _native as N
-from ._native import ACT_NONE, ACT_RELU, PRO_AFFINE, PRO_AFFINE_RELU, PRO_NONE, PRO_RELU  # noqa: F401
+from ._native import ACT_NONE, ACT_PRELU, ACT_RELU, PRO_AFFINE, PRO_AFFINE_RELU, PRO_NONE, PRO_RELU  # noqa: F401
 
 __all__ = [
     "pack_weight", "conv", "conv_wgrad", "to_view", "from_view", "relu_bwd", "add",
     "loss_fwd", "loss_bwd", "psnr", "workspace", "LOSS_KINDS",
     "bn_stats", "bn_finalize", "bn_fold_running", "bn_relu_bwd_reduce", "bn_relu_bwd_apply",
     "duf_dynfilter_fwd", "duf_dynfilter_bwd",
+    "subpixel_conv_weight", "subpixel_wgrad_fold", "prelu_wgrad", "prelu_bwd",
 ]
 
 LOSS_KINDS = {"L1Loss": 0, "MSELoss": 1, "HuberLoss": 2, "CharbonnierLoss": 3}
@@ -94,22 +95,30 @@ def pack_weight(w: torch.Tensor, mode: int, dtype: torch.dtype, perm_r: int = 1)
     return out
 
 
-def _desc(k, pad, prologue=PRO_NONE, act=ACT_NONE, out_scale=1.0, accumulate=False, bias_r=1) -> N.ConvDesc:
+def _desc(k, pad, prologue=PRO_NONE, act=ACT_NONE, out_scale=1.0, accumulate=False, bias_r=1,
+          act_param=None, mask_slope=None) -> N.ConvDesc:
     kd, kh, kw = k
     pd, ph, pw = pad
-    return N.ConvDesc(kd, kh, kw, pd, ph, pw, prologue, act, float(out_scale), 1 if accumulate else 0, bias_r)
+    return N.ConvDesc(kd, kh, kw, pd, ph, pw, prologue, act, float(out_scale), 1 if accumulate else 0, bias_r,
+                      N.ptr(act_param), N.ptr(mask_slope))
 
 
 def conv(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, *, bias: torch.Tensor | None = None,
          prologue: int = PRO_NONE, pro_scale: torch.Tensor | None = None, pro_shift: torch.Tensor | None = None,
          act: int = ACT_NONE, out_scale: float = 1.0, accumulate: bool = False,
          residual: torch.Tensor | None = None, mask: torch.Tensor | None = None,
-         x_shuffle: int = 1, y_shuffle: int = 1) -> torch.Tensor:
+         x_shuffle: int = 1, y_shuffle: int = 1, act_param: torch.Tensor | None = None,
+         mask_slope: torch.Tensor | None = None, bias_r: int | None = None) -> torch.Tensor:
     """y[...] = epilogue(conv(prologue(x), W) + bias); writes into the given y view.
 
-    residual/mask are views with y's logical shape (and y_shuffle addressing)."""
+    residual/mask are views with y's logical shape (and y_shuffle addressing).
+    act=ACT_PRELU reads its slope from the device scalar act_param; with
+    mask_slope the mask keeps mask_slope * value where mask <= 0 (PReLU
+    backward) instead of zero (ReLU backward).  bias_r overrides the bias
+    order (default: torch pixel-shuffle order of a y_shuffle output)."""
     lib = _lib()
-    d = _desc(k, pad, prologue, act, out_scale, accumulate, y_shuffle if bias is not None else 1)
+    br = bias_r if bias_r is not None else (y_shuffle if bias is not None else 1)
+    d = _desc(k, pad, prologue, act, out_scale, accumulate, br, act_param, mask_slope)
     xv = N.t5(x, x_shuffle)
     yv = N.t5(y, y_shuffle)
     rv = N.t5(residual, y_shuffle) if residual is not None else None
@@ -321,3 +330,61 @@ def duf_dynfilter_bwd(x: torch.Tensor, logits: torch.Tensor, gout: torch.Tensor,
                                        dr.data_ptr(), N.dtype_code(dtype), N.stream_ptr(x.device)),
             "duf_dynfilter_bwd")
     return dl, dr
+
+
+# ------------------------------------------------------- DRF (sub-pixel, PReLU) --
+def subpixel_conv_weight(w: torch.Tensor, bias: torch.Tensor | None, k: int, s: int, p: int, transposed: bool):
+    """Equivalent 3x3 conv weight/bias (fp32, torch layout, view channel order)
+    of nn.Conv2d / nn.ConvTranspose2d(k, stride s, padding p) on the sub-pixel grid."""
+    lib = _lib()
+    if transposed:
+        cin, cout = w.shape[:2]
+        weq = torch.empty((s * s * cout, cin, 3, 3), dtype=torch.float32, device=w.device)
+        beq = torch.empty(s * s * cout, dtype=torch.float32, device=w.device)
+    else:
+        cout, cin = w.shape[:2]
+        weq = torch.empty((cout, s * s * cin, 3, 3), dtype=torch.float32, device=w.device)
+        beq = torch.empty(cout, dtype=torch.float32, device=w.device)
+    wc = w.detach().float().contiguous()
+    bc = bias.detach().float().contiguous() if bias is not None else None
+    N.check(lib.vsrk_subpixel_conv_weight(wc.data_ptr(), N.ptr(bc), cin, cout, k, s, p, 1 if transposed else 0,
+                                          weq.data_ptr(), beq.data_ptr(), N.stream_ptr(w.device)),
+            "subpixel_conv_weight")
+    return weq, beq
+
+
+def subpixel_wgrad_fold(dweq: torch.Tensor, dbeq: torch.Tensor | None, dw: torch.Tensor, db: torch.Tensor | None,
+                        k: int, s: int, p: int, transposed: bool, accumulate: bool = False) -> None:
+    lib = _lib()
+    if transposed:
+        cin, cout = dw.shape[:2]
+    else:
+        cout, cin = dw.shape[:2]
+    assert dw.dtype == torch.float32 and dw.is_contiguous()
+    N.check(lib.vsrk_subpixel_wgrad_fold(dweq.data_ptr(), N.ptr(dbeq), cin, cout, k, s, p, 1 if transposed else 0,
+                                         dw.data_ptr(), N.ptr(db), 1 if accumulate else 0, N.stream_ptr(dw.device)),
+            "subpixel_wgrad_fold")
+
+
+def prelu_wgrad(y: torch.Tensor, dx: torch.Tensor, a: torch.Tensor, da: torch.Tensor, accumulate: bool) -> None:
+    """da [+]= sum_{y<0} dx * y / a^2 (nn.PReLU slope gradient from output and input gradient)."""
+    lib = _lib()
+    nb = lib.vsrk_prelu_workspace_size()
+    ws = workspace(nb, y.device)
+    yv, dv = N.t5(y), N.t5(dx)
+    N.check(lib.vsrk_prelu_wgrad(C.byref(yv), C.byref(dv), a.data_ptr(), da.data_ptr(), 1 if accumulate else 0,
+                                 ws.data_ptr(), ws.numel(), N.stream_ptr(y.device)), "prelu_wgrad")
+
+
+def prelu_bwd(y: torch.Tensor, dy: torch.Tensor, a: torch.Tensor, dx: torch.Tensor, da: torch.Tensor,
+              accumulate_da: bool, dy2: torch.Tensor | None = None) -> torch.Tensor:
+    """dx = (dy [+ dy2]) * (y > 0 ? 1 : a); da [+]= sum_{y<0} dx*y/a^2 (one pass)."""
+    lib = _lib()
+    nb = lib.vsrk_prelu_workspace_size()
+    ws = workspace(nb, y.device)
+    yv, gv, ov = N.t5(y), N.t5(dy), N.t5(dx)
+    g2 = N.t5(dy2) if dy2 is not None else None
+    N.check(lib.vsrk_prelu_bwd(C.byref(yv), C.byref(gv), C.byref(g2) if g2 is not None else None, a.data_ptr(),
+                               C.byref(ov), da.data_ptr(), 1 if accumulate_da else 0, ws.data_ptr(), ws.numel(),
+                               N.stream_ptr(y.device)), "prelu_bwd")
+    return dx
