@@ -76,7 +76,8 @@ def _psnr(out, hr):
     return psnr_denorm(out, hr, "acdc")
 
 
-CASES = ["edsr_x4_small", "edsr_x3_small", "edsr_x2_cfg1", "edsr_x4_canon", "duf_x4_canon"]
+CASES = ["edsr_x4_small", "edsr_x3_small", "edsr_x2_cfg1", "edsr_x4_canon", "duf_x4_canon", "drf_x4_canon",
+         "drf_sisr_x2_small"]
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])

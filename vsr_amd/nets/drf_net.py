@@ -1,0 +1,398 @@
+"""DRF (Deep Recurrent Feedback) generators on fused HIP kernels.
+
+Same constructors, module trees and state_dict keys as the reference
+DRFNet (src/model/nets/drf_net.py:8-147, VSR: list of T frames -> list of T
+outputs) and DRFSISRNet (src/model/nets/drf_sisr_net.py:8-50, SISR: one image
+fed num_steps times -> list of num_steps outputs), built in the same order so
+one seed gives the same initial weights:
+
+    in_block.{conv1, prelu1, conv2, prelu2}                    (drf_net.py:52-58)
+    f_block.in_block.{conv, prelu}                              (:64-66)
+    f_block.up_blocks.{0: deconv, prelu | i: conv1, prelu1, deconv2, prelu2}
+    f_block.down_blocks.{0: conv, prelu | i: conv1, prelu1, conv2, prelu2}  (:78-102)
+    f_block.out_block.{conv, prelu}                             (:104-106)
+    out_block.{conv1, pixelshuffle1, ..., conv<n>}              (:136-147)
+
+How it runs (one HIP conv launch per reference conv, PReLU fused into its
+epilogue):
+  * Concatenations are never materialised: [in_features, hidden] (X0), the
+    low-res feature list (L, (G+1)*F channels) and the high-res feature list
+    (Hc, G*F channels) are preallocated channels-last buffers; every conv
+    writes its channel slice and consumers read channel-prefix views.
+  * The feedback hidden state of frame t is written by f_block.out_block's
+    conv straight into X0 of frame t+1.
+  * ConvTranspose2d / Conv2d(k, stride s, pad p) are 3x3 sub-pixel convs
+    (vsrk_subpixel_conv_weight): the deconv writes through a shuffle-s view
+    of its Hc slice, the strided conv reads its high-res input through one.
+  * Backward is hand-written (frames in reverse): every PReLU output's
+    gradient is accumulated from all its consumers into the matching slice of
+    a gradient buffer of the concat layout, then one fused pass applies the
+    PReLU derivative and reduces its slope gradient; conv weight gradients of
+    the weights shared by all frames accumulate across frames.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import functional as F
+from .base_net import BaseNet
+
+K1, P0 = (1, 1, 1), (0, 0, 0)
+K3, P1 = (1, 3, 3), (0, 1, 1)
+_PROJ = {2: (6, 2, 2), 3: (7, 3, 2), 4: (8, 4, 2), 8: (12, 8, 2)}  # drf_net.py:70-77
+
+
+def _prelu():
+    return nn.PReLU(num_parameters=1, init=0.2)
+
+
+class _InBlock(nn.Sequential):
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.add_module("conv1", nn.Conv2d(in_channels, 4 * out_channels, kernel_size=3, padding=1))
+        self.add_module("prelu1", _prelu())
+        self.add_module("conv2", nn.Conv2d(4 * out_channels, out_channels, kernel_size=1))
+        self.add_module("prelu2", _prelu())
+
+
+class _FBlock(nn.Module):
+    def __init__(self, num_features, num_groups, upscale_factor):
+        super().__init__()
+        f = num_features
+        self.in_block = nn.Sequential()
+        self.in_block.add_module("conv", nn.Conv2d(f * 2, f, kernel_size=1))
+        self.in_block.add_module("prelu", _prelu())
+        self.up_blocks = nn.ModuleList()
+        self.down_blocks = nn.ModuleList()
+        k, s, p = _PROJ[upscale_factor]
+        for i in range(num_groups):
+            up, down = nn.Sequential(), nn.Sequential()
+            if i == 0:
+                up.add_module("deconv", nn.ConvTranspose2d(f, f, kernel_size=k, stride=s, padding=p))
+                up.add_module("prelu", _prelu())
+                self.up_blocks.append(up)
+                down.add_module("conv", nn.Conv2d(f, f, kernel_size=k, stride=s, padding=p))
+                down.add_module("prelu", _prelu())
+                self.down_blocks.append(down)
+            else:
+                up.add_module("conv1", nn.Conv2d(f * (i + 1), f, kernel_size=1))
+                up.add_module("prelu1", _prelu())
+                up.add_module("deconv2", nn.ConvTranspose2d(f, f, kernel_size=k, stride=s, padding=p))
+                up.add_module("prelu2", _prelu())
+                self.up_blocks.append(up)
+                down.add_module("conv1", nn.Conv2d(f * (i + 1), f, kernel_size=1))
+                down.add_module("prelu1", _prelu())
+                down.add_module("conv2", nn.Conv2d(f, f, kernel_size=k, stride=s, padding=p))
+                down.add_module("prelu2", _prelu())
+                self.down_blocks.append(down)
+        self.out_block = nn.Sequential()
+        self.out_block.add_module("conv", nn.Conv2d(f * num_groups, f, kernel_size=1))
+        self.out_block.add_module("prelu", _prelu())
+        self._hidden_state = None
+
+    @property
+    def hidden_state(self):  # API parity (drf_net.py:110-116); the fused path keeps it in X0 buffers
+        return self._hidden_state
+
+    @hidden_state.setter
+    def hidden_state(self, state):
+        self._hidden_state = state
+
+
+def _up_steps(r: int) -> list[int]:
+    if math.log(r, 2) % 1 == 0:
+        return [2] * int(math.log(r, 2))
+    if r == 3:
+        return [3]
+    raise ValueError(f"upscale factor {r}")
+
+
+class _OutBlock(nn.Sequential):
+    def __init__(self, in_channels, out_channels, upscale_factor):
+        super().__init__()
+        steps = _up_steps(upscale_factor)
+        for i, s in enumerate(steps):
+            self.add_module(f"conv{i + 1}", nn.Conv2d(in_channels, s * s * in_channels, kernel_size=3, padding=1))
+            self.add_module(f"pixelshuffle{i + 1}", nn.PixelShuffle(s))
+        self.add_module(f"conv{len(steps) + 1}", nn.Conv2d(in_channels, out_channels, kernel_size=3, padding=1))
+
+
+class _DRFBase(BaseNet):
+    def __init__(self, in_channels, out_channels, num_features, num_groups, upscale_factor):
+        super().__init__()
+        self.in_channels = in_channels
+        self.out_channels = out_channels
+        self.num_features = num_features
+        self.num_groups = num_groups
+        if upscale_factor not in [2, 3, 4, 8]:
+            raise ValueError(f"The upscale factor should be 2, 3, 4 or 8. Got {upscale_factor}.")
+        self.upscale_factor = upscale_factor
+        self.in_block = _InBlock(in_channels, num_features)
+        self.f_block = _FBlock(num_features, num_groups, upscale_factor)
+        self.out_block = _OutBlock(num_features, out_channels, upscale_factor)
+
+    def _returns_list(self) -> bool:
+        return True
+
+    def _frames(self, inputs) -> list:
+        raise NotImplementedError
+
+    # -- weights prepared once per forward (shared by all frames and the backward)
+    def _packer(self):
+        cd = self.compute_dtype
+        cache: dict = {}
+
+        def pw(conv, mode=0, perm_r=1):
+            key = ("w", id(conv.weight), mode, perm_r)
+            if key not in cache:
+                cache[key] = F.pack_weight(conv.weight, mode, cd, perm_r=perm_r)
+            return cache[key]
+
+        def sp(conv, transposed, mode=0):
+            k, s, p = _PROJ[self.upscale_factor]
+            key = ("eq", id(conv.weight))
+            if key not in cache:
+                cache[key] = F.subpixel_conv_weight(conv.weight, conv.bias, k, s, p, transposed)
+            weq, beq = cache[key]
+            pkey = ("sp", id(conv.weight), mode)
+            if pkey not in cache:
+                cache[pkey] = F.pack_weight(weq, mode, cd)
+            return cache[pkey], beq
+
+        return pw, sp
+
+    def _ups(self):
+        steps = _up_steps(self.upscale_factor)
+        return [(getattr(self.out_block, f"conv{j}"), s) for j, s in enumerate(steps, start=1)]
+
+    def _last_conv(self):
+        return getattr(self.out_block, f"conv{len(_up_steps(self.upscale_factor)) + 1}")
+
+    # ------------------------------------------------------------------
+    def _run(self, inputs, tape: dict | None):
+        frames = self._frames(inputs)
+        cd = self.compute_dtype
+        f, G = self.num_features, self.num_groups
+        k, s, p = _PROJ[self.upscale_factor]
+        b, cin, h, w = frames[0].shape
+        dev = frames[0].device
+        H, W = h * s, w * s
+        PR = F.ACT_PRELU
+        pw, sp = self._packer()
+        ib, fb = self.in_block, self.f_block
+
+        def new(hh, ww, c):
+            return torch.empty((b, 1, hh, ww, c), dtype=cd, device=dev)
+
+        outs, recs = [], []
+        X0 = new(h, w, 2 * f)
+        for t, x in enumerate(frames):
+            xv = F.to_view(x, cd, cpad=8)[..., :cin]
+            u1 = new(h, w, 4 * f)
+            F.conv(xv, pw(ib.conv1), u1, K3, P1, bias=ib.conv1.bias, act=PR, act_param=ib.prelu1.weight)
+            F.conv(u1, pw(ib.conv2), X0[..., :f], K1, P0, bias=ib.conv2.bias, act=PR, act_param=ib.prelu2.weight)
+            if t == 0:  # hidden_state = in_features (drf_net.py:42-43)
+                F.conv(u1, pw(ib.conv2), X0[..., f:], K1, P0, bias=ib.conv2.bias, act=PR,
+                       act_param=ib.prelu2.weight)
+            L = new(h, w, (G + 1) * f)
+            F.conv(X0, pw(fb.in_block.conv), L[..., :f], K1, P0, bias=fb.in_block.conv.bias, act=PR,
+                   act_param=fb.in_block.prelu.weight)
+            Hc = new(H, W, G * f)
+            t1s, t2s = [None] * G, [None] * G
+            for i in range(G):
+                up, dn = fb.up_blocks[i], fb.down_blocks[i]
+                if i == 0:
+                    src, dec, dpr = L[..., :f], up.deconv, up.prelu
+                else:
+                    src = new(h, w, f)
+                    F.conv(L[..., :(i + 1) * f], pw(up.conv1), src, K1, P0, bias=up.conv1.bias, act=PR,
+                           act_param=up.prelu1.weight)
+                    t1s[i], dec, dpr = src, up.deconv2, up.prelu2
+                wq, bq = sp(dec, True)
+                F.conv(src, wq, Hc[..., i * f:(i + 1) * f], K3, P1, bias=bq, bias_r=1, y_shuffle=s, act=PR,
+                       act_param=dpr.weight)
+                if i == 0:
+                    hsrc, cv, cpr = Hc[..., :f], dn.conv, dn.prelu
+                else:
+                    hsrc = new(H, W, f)
+                    F.conv(Hc[..., :(i + 1) * f], pw(dn.conv1), hsrc, K1, P0, bias=dn.conv1.bias, act=PR,
+                           act_param=dn.prelu1.weight)
+                    t2s[i], cv, cpr = hsrc, dn.conv2, dn.prelu2
+                wq, bq = sp(cv, False)
+                F.conv(hsrc, wq, L[..., (i + 1) * f:(i + 2) * f], K3, P1, bias=bq, x_shuffle=s, act=PR,
+                       act_param=cpr.weight)
+            X0n = new(h, w, 2 * f)
+            ffeat = X0n[..., f:]  # f_features = next frame's hidden state (drf_net.py:45)
+            F.conv(L[..., f:], pw(fb.out_block.conv), ffeat, K1, P0, bias=fb.out_block.conv.bias, act=PR,
+                   act_param=fb.out_block.prelu.weight)
+            feat = F.add(X0[..., :f], ffeat, new(h, w, f))  # global residual skip (drf_net.py:46)
+            u, hh, ww, ups_in = feat, h, w, []
+            for conv, st in self._ups():
+                nxt = new(hh * st, ww * st, f)
+                F.conv(u, pw(conv, perm_r=st), nxt, K3, P1, bias=conv.bias, y_shuffle=st)
+                ups_in.append(u)
+                u, hh, ww = nxt, hh * st, ww * st
+            tc = self._last_conv()
+            co = self.out_channels
+            if co == 1:
+                y = torch.empty((b, 1, hh, ww), dtype=torch.float32, device=dev)
+                F.conv(u, pw(tc), y.view(b, 1, hh, ww, 1), K3, P1, bias=tc.bias)
+            else:
+                tmp = torch.empty((b, 1, hh, ww, co), dtype=torch.float32, device=dev)
+                y = F.from_view(F.conv(u, pw(tc), tmp, K3, P1, bias=tc.bias))
+            outs.append(y)
+            if tape is not None:
+                recs.append(dict(xv=xv, u1=u1, X0=X0, L=L, Hc=Hc, t1s=t1s, t2s=t2s, ffeat=ffeat, ups_in=ups_in,
+                                 tail_in=u))
+            X0 = X0n
+        if tape is not None:
+            tape.update(recs=recs, shape=(b, h, w), packer=(pw, sp))
+        return outs
+
+    def _backward(self, tape: dict, gys) -> dict:
+        cd = self.compute_dtype
+        f, G = self.num_features, self.num_groups
+        k, s, p = _PROJ[self.upscale_factor]
+        b, h, w = tape["shape"]
+        H, W = h * s, w * s
+        pw, sp = tape["packer"]
+        ib, fb = self.in_block, self.f_block
+        recs = tape["recs"]
+        dev = recs[0]["X0"].device
+        if not isinstance(gys, (tuple, list)):
+            gys = [gys]
+        grads: dict = {}
+        bufs: dict = {}  # id(param) -> gradient buffer (accumulated over frames)
+
+        def new(hh, ww, c):
+            return torch.empty((b, 1, hh, ww, c), dtype=cd, device=dev)
+
+        def zeros(hh, ww, c):
+            return torch.zeros((b, 1, hh, ww, c), dtype=cd, device=dev)
+
+        def gbuf(prm):
+            key = id(prm)
+            if key in bufs:
+                return bufs[key][1], True
+            g = self._grad_buffer(prm)
+            bufs[key] = (prm, g)
+            return g, False
+
+        def wgrad(conv, x, dy, ksz, pad, **kw):
+            dw, acc = gbuf(conv.weight)
+            db, _ = gbuf(conv.bias)
+            F.conv_wgrad(x, dy, ksz, pad, dw.view(*dw.shape[:2], 1, *dw.shape[2:]), db, accumulate=acc, **kw)
+
+        def sp_wgrad(conv, x, dy, transposed):
+            k_, s_, p_ = k, s, p
+            cop = s_ * s_ * f if transposed else f
+            cip = f if transposed else s_ * s_ * f
+            dweq = torch.empty((cop, cip, 1, 3, 3), dtype=torch.float32, device=dev)
+            dbeq = torch.empty(cop, dtype=torch.float32, device=dev)
+            if transposed:
+                F.conv_wgrad(x, dy, K3, P1, dweq, dbeq, dy_shuffle=s_)
+            else:
+                F.conv_wgrad(x, dy, K3, P1, dweq, dbeq, x_shuffle=s_)
+            dw, acc = gbuf(conv.weight)
+            db, _ = gbuf(conv.bias)
+            F.subpixel_wgrad_fold(dweq, dbeq, dw, db, k_, s_, p_, transposed, accumulate=acc)
+
+        def prelu(y, dy, pr, out, dy2=None):
+            da, acc = gbuf(pr.weight)
+            return F.prelu_bwd(y, dy, pr.weight, out, da, acc, dy2=dy2)
+
+        d_hidden = None  # grad of the previous frame's f_features (X0_t[..., f:])
+        for t in range(len(recs) - 1, -1, -1):
+            rc = recs[t]
+            gy = gys[t] if t < len(gys) and gys[t] is not None else None
+            u = rc["tail_in"]
+            hh, ww = u.shape[2], u.shape[3]
+            co = self.out_channels
+            if gy is None:
+                gy = torch.zeros((b, co, hh, ww), dtype=torch.float32, device=dev)
+            g = F.to_view(gy, cd, cpad=8)[..., :co]
+            tc = self._last_conv()
+            wgrad(tc, u, g, K3, P1)
+            du = F.conv(g, pw(tc, 1), new(hh, ww, f), K3, P1)
+            for (conv, st), uin in reversed(list(zip(self._ups(), rc["ups_in"]))):
+                wgrad(conv, uin, du, K3, P1, perm_r=st, dy_shuffle=st)
+                hh, ww = hh // st, ww // st
+                du = F.conv(du, pw(conv, 1, perm_r=st), new(hh, ww, f), K3, P1, x_shuffle=st)
+            gfeat = du  # grad of features = in_features + f_features
+            L, Hc, X0 = rc["L"], rc["Hc"], rc["X0"]
+            # f_block out: f_features feeds the skip and the next frame's hidden state
+            gout = prelu(rc["ffeat"], gfeat, fb.out_block.prelu, new(h, w, f), dy2=d_hidden)
+            wgrad(fb.out_block.conv, L[..., f:], gout, K1, P0)
+            dL = zeros(h, w, (G + 1) * f)
+            dHc = zeros(H, W, G * f)
+            F.conv(gout, pw(fb.out_block.conv, 1), dL[..., f:], K1, P0, accumulate=True)
+            for i in range(G - 1, -1, -1):
+                up, dn = fb.up_blocks[i], fb.down_blocks[i]
+                # down projection -> lr_{i+1} = L[..., (i+1)f:(i+2)f]
+                cv, cpr = (dn.conv, dn.prelu) if i == 0 else (dn.conv2, dn.prelu2)
+                sl = slice((i + 1) * f, (i + 2) * f)
+                gl = prelu(L[..., sl], dL[..., sl], cpr, new(h, w, f))
+                hsrc = Hc[..., :f] if i == 0 else rc["t2s"][i]
+                sp_wgrad(cv, hsrc, gl, transposed=False)
+                wq1, _ = sp(cv, False, 1)
+                if i == 0:
+                    F.conv(gl, wq1, dHc[..., :f], K3, P1, y_shuffle=s, accumulate=True)
+                else:
+                    dt2 = F.conv(gl, wq1, new(H, W, f), K3, P1, y_shuffle=s)
+                    prelu(rc["t2s"][i], dt2, dn.prelu1, dt2)
+                    wgrad(dn.conv1, Hc[..., :(i + 1) * f], dt2, K1, P0)
+                    F.conv(dt2, pw(dn.conv1, 1), dHc[..., :(i + 1) * f], K1, P0, accumulate=True)
+                # up projection -> hr_i = Hc[..., i f:(i+1) f]
+                dec, dpr = (up.deconv, up.prelu) if i == 0 else (up.deconv2, up.prelu2)
+                sh = slice(i * f, (i + 1) * f)
+                gh = prelu(Hc[..., sh], dHc[..., sh], dpr, new(H, W, f))
+                src = L[..., :f] if i == 0 else rc["t1s"][i]
+                sp_wgrad(dec, src, gh, transposed=True)
+                wq1, _ = sp(dec, True, 1)
+                if i == 0:
+                    F.conv(gh, wq1, dL[..., :f], K3, P1, x_shuffle=s, accumulate=True)
+                else:
+                    dt1 = F.conv(gh, wq1, new(h, w, f), K3, P1, x_shuffle=s)
+                    prelu(rc["t1s"][i], dt1, up.prelu1, dt1)
+                    wgrad(up.conv1, L[..., :(i + 1) * f], dt1, K1, P0)
+                    F.conv(dt1, pw(up.conv1, 1), dL[..., :(i + 1) * f], K1, P0, accumulate=True)
+            g0 = prelu(L[..., :f], dL[..., :f], fb.in_block.prelu, new(h, w, f))
+            wgrad(fb.in_block.conv, X0, g0, K1, P0)
+            dX0 = F.conv(g0, pw(fb.in_block.conv, 1), new(h, w, 2 * f), K1, P0)
+            if t == 0:  # the first hidden state is in_features itself
+                F.add(dX0[..., :f], dX0[..., f:], dX0[..., :f])
+                d_hidden = None
+            else:
+                d_hidden = dX0[..., f:]
+            gin = prelu(X0[..., :f], gfeat, ib.prelu2, new(h, w, f), dy2=dX0[..., :f])
+            wgrad(ib.conv2, rc["u1"], gin, K1, P0)
+            du1 = F.conv(gin, pw(ib.conv2, 1), new(h, w, 4 * f), K1, P0)
+            prelu(rc["u1"], du1, ib.prelu1, du1)
+            wgrad(ib.conv1, rc["xv"], du1, K3, P1)
+        for prm, g in bufs.values():
+            self._grad_done(grads, prm, g)
+        return grads
+
+
+class DRFNet(_DRFBase):
+    """Deep Recurrent Feedback Network, VSR (drf_net.py:8-49): list of T (B,C,h,w) -> list of T (B,C,rh,rw)."""
+
+    def _frames(self, inputs):
+        return list(inputs)
+
+    def forward(self, inputs):
+        return super().forward(list(inputs))
+
+
+class DRFSISRNet(_DRFBase):
+    """DRFN for SISR (drf_sisr_net.py:8-50): (B,C,h,w) -> list of num_steps (B,C,rh,rw)."""
+
+    def __init__(self, in_channels, out_channels, num_steps, num_features, num_groups, upscale_factor):
+        super().__init__(in_channels, out_channels, num_features, num_groups, upscale_factor)
+        self.num_steps = num_steps
+
+    def _frames(self, inputs):
+        return [inputs] * self.num_steps
