@@ -190,6 +190,17 @@ int vsrk_psnr(const float* out, const float* target, int32_t batch, int64_t per_
               float mean, float std, float max_value, float* psnr_per_sample, float* psnr_mean, void* workspace,
               size_t workspace_bytes, void* stream);
 
+/* [Denormalize +] SSIM (utils.py:1-20 then metrics.py:39-113, dim = 2): out and
+ * target are (batch, channels, h, w) fp32 contiguous, h, w >= 11.  Per image
+ * the five depthwise 11x11 Gaussian moments (valid convolution), the SSIM map
+ * (c1 = (0.01 range)^2, c2 = (0.03 range)^2) and its mean: writes the
+ * per-sample means (SSIM(size_average=False)) and their mean (size_average
+ * = True).  Workspace: vsrk_ssim_workspace_size(). */
+size_t vsrk_ssim_workspace_size(int32_t batch, int32_t channels, int32_t h, int32_t w);
+int vsrk_ssim(const float* out, const float* target, int32_t batch, int32_t channels, int32_t h, int32_t w,
+              int32_t denormalize, float mean, float std, float value_range, float* ssim_per_sample, float* ssim_mean,
+              void* workspace, size_t workspace_bytes, void* stream);
+
 /* BatchNorm3d, training statistics (duf_net.py:116,198,201,209,212).  Split
  * so a data-parallel caller can all-reduce the per-channel sums between the
  * calls (SyncBatchNorm):

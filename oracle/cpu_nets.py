@@ -38,6 +38,30 @@ def psnr(output: torch.Tensor, target: torch.Tensor, max_value: float = 255.0, s
     return val.mean() if size_average else val
 
 
+def ssim(output: torch.Tensor, target: torch.Tensor, dim: int = 2, channels: int = 1, size_average: bool = True,
+         value_range: float = 255.0) -> torch.Tensor:
+    """metrics.py:39-113 restated: depthwise Gaussian window exp(-((x-mu)/(2*sigma))^2)
+    (11 taps, sigma 1.5, product over dims, normalised), valid convolution,
+    SSIM map, mean (or per-sample mean)."""
+    c1, c2 = (0.01 * value_range) ** 2, (0.03 * value_range) ** 2
+    conv = Fn.conv2d if dim == 2 else Fn.conv3d
+    grids = torch.meshgrid([torch.arange(11, dtype=torch.float32) for _ in range(dim)], indexing="ij")
+    kernel = 1
+    for g in grids:
+        kernel = kernel * (1 / (1.5 * math.sqrt(2 * math.pi)) * torch.exp(-((g - 5) / (2 * 1.5)) ** 2))
+    kernel = (kernel / torch.sum(kernel)).view(1, 1, *kernel.shape).repeat(channels, *[1] * (dim + 1))
+    kernel = kernel.to(output.dtype)
+    mu1 = conv(output, weight=kernel, groups=channels)
+    mu2 = conv(target, weight=kernel, groups=channels)
+    s1 = conv(output * output, weight=kernel, groups=channels) - mu1.pow(2)
+    s2 = conv(target * target, weight=kernel, groups=channels) - mu2.pow(2)
+    s12 = conv(output * target, weight=kernel, groups=channels) - mu1 * mu2
+    m = ((2 * mu1 * mu2 + c1) * (2.0 * s12 + c2)) / ((mu1.pow(2) + mu2.pow(2) + c1) * (s1 + s2 + c2))
+    if size_average:
+        return m.mean()
+    return m.mean(dim=list(range(1, output.dim())))
+
+
 def _pow2_steps(r: int):
     if (math.log(r, 2) % 1) == 0:
         return [2] * int(math.log(r, 2))

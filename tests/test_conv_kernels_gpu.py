@@ -222,3 +222,133 @@ def test_conv_epilogue_combos(dtype, combo, shape):
            residual=res.to(DEV, dtype) if "res" in parts else None, accumulate="acc" in parts)
     err = (yd.double().cpu() - ref).abs().max().item()
     assert err <= _tol(dtype, ref) * 2, err
+
+
+# Thin-channel kernels (conv_thin.hip): cin <= 4 (im2col k = (tap, c)) and
+# cout <= 3 (m = (tap, co)), bf16 inputs, with every epilogue form; inputs in
+# the nets' 8-channel padded storage as well as plain contiguous views.
+THIN_FWD = [
+    # (N, D, H, W, Cin, Cout, k, pad, padded_storage)
+    (2, 1, 20, 45, 1, 64, (1, 3, 3), (0, 1, 1), True),
+    (2, 1, 12, 33, 3, 48, (1, 3, 3), (0, 1, 1), False),
+    (2, 4, 9, 40, 1, 32, (3, 3, 3), (1, 1, 1), True),
+    (1, 1, 9, 35, 2, 256, (1, 3, 3), (0, 1, 1), False),
+    (2, 3, 7, 19, 1, 40, (1, 1, 1), (0, 0, 0), True),
+    (2, 1, 20, 70, 64, 1, (1, 3, 3), (0, 1, 1), False),
+    (2, 1, 9, 33, 32, 3, (1, 3, 3), (0, 1, 1), False),
+    (2, 2, 9, 33, 96, 2, (1, 1, 1), (0, 0, 0), False),
+]
+
+
+def _thin_input(x, padded):
+    if not padded:
+        return x.to(DEV, torch.bfloat16)
+    st = torch.zeros((*x.shape[:-1], 8), dtype=torch.bfloat16, device=DEV)
+    st[..., :x.shape[-1]] = x.to(DEV, torch.bfloat16)
+    return st[..., :x.shape[-1]]
+
+
+@pytest.mark.parametrize("ydtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", THIN_FWD)
+def test_thin_conv_forward(case, ydtype):
+    n, d, h, w, ci, co, k, pad, padded = case
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn((n, d, h, w, ci), generator=g)
+    wt = torch.randn((co, ci, *k), generator=g) / (ci * k[0] * k[1] * k[2]) ** 0.5
+    b = torch.randn(co, generator=g)
+    do = d + 2 * pad[0] - k[0] + 1
+    ref = _ref_conv(_q(x, torch.bfloat16), _q(wt, torch.bfloat16), b.double(), pad)
+    y = torch.empty((n, do, h, w, co), dtype=ydtype, device=DEV)
+    F.conv(_thin_input(x, padded), F.pack_weight(wt.to(DEV), 0, torch.bfloat16), y, k, pad, bias=b.to(DEV))
+    err = (y.double().cpu() - ref).abs().max().item()
+    assert err <= _tol(torch.bfloat16, ref), err
+
+
+@pytest.mark.parametrize("case", [THIN_FWD[0], THIN_FWD[2], THIN_FWD[5], THIN_FWD[6]])
+def test_thin_conv_fused(case):
+    """prologue (BN-affine+ReLU), PReLU, out_scale, mask with slope, residual, accumulate."""
+    n, d, h, w, ci, co, k, pad, padded = case
+    g = torch.Generator().manual_seed(22)
+    do = d + 2 * pad[0] - k[0] + 1
+    x = torch.randn((n, d, h, w, ci), generator=g)
+    wt = torch.randn((co, ci, *k), generator=g) / (ci * k[0] * k[1] * k[2]) ** 0.5
+    b = torch.randn(co, generator=g)
+    sc = torch.rand(ci, generator=g) + 0.5
+    sh = torch.randn(ci, generator=g)
+    slope = torch.tensor([0.25])
+    mslope = torch.tensor([0.3])
+    mask = torch.randn((n, do, h, w, co), generator=g)
+    res = torch.randn((n, do, h, w, co), generator=g)
+    y0 = torch.randn((n, do, h, w, co), generator=g)
+    bf = torch.bfloat16
+    xin = torch.relu(_q(x, bf) * sc.double() + sh.double()).to(bf).double()
+    t = _ref_conv(xin, _q(wt, bf), b.double(), pad) * 0.5
+    t = torch.where(t > 0, t, 0.25 * t)
+    t = torch.where(_q(mask, bf) > 0, t, 0.3 * t)
+    ref = t + _q(res, bf) + _q(y0, bf)
+    yd = y0.to(DEV, bf)
+    F.conv(_thin_input(x, padded), F.pack_weight(wt.to(DEV), 0, bf), yd, k, pad, bias=b.to(DEV),
+           prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV), act=F.ACT_PRELU,
+           act_param=slope.to(DEV), out_scale=0.5, mask=mask.to(DEV, bf), mask_slope=mslope.to(DEV),
+           residual=res.to(DEV, bf), accumulate=True)
+    err = (yd.double().cpu() - ref).abs().max().item()
+    assert err <= _tol(bf, ref) * 2, err
+
+
+@pytest.mark.parametrize("case", [(2, 1, 20, 70, 64, 1, (1, 3, 3), (0, 1, 1)),
+                                  (2, 1, 9, 33, 32, 3, (1, 3, 3), (0, 1, 1)),
+                                  (2, 2, 11, 40, 16, 2, (1, 1, 1), (0, 0, 0)),
+                                  (1, 1, 13, 37, 128, 1, (1, 3, 3), (0, 1, 1))])
+@pytest.mark.parametrize("prologue", [False, True])
+def test_thin_wgrad(case, prologue):
+    """weight/bias gradient of a cout <= 3 conv (the tail conv) against fp64 autograd."""
+    n, d, h, w, ci, co, k, pad = case
+    bf = torch.bfloat16
+    g = torch.Generator().manual_seed(23)
+    x = torch.randn((n, d, h, w, ci), generator=g)
+    gy = torch.randn((n, d, h, w, co), generator=g)
+    wt = torch.randn((co, ci, *k), generator=g) / 12
+    sc = torch.rand(ci, generator=g) + 0.5
+    sh = torch.randn(ci, generator=g)
+    xin = _q(x, bf)
+    if prologue:
+        xin = torch.relu(xin * sc.double() + sh.double()).to(bf).double()
+    wr = _q(wt, bf).requires_grad_(True)
+    br = torch.zeros(co, dtype=torch.float64, requires_grad=True)
+    _ref_conv(xin, wr, br, pad).backward(_q(gy, bf))
+    dw = torch.empty((co, ci, *k), device=DEV)
+    db = torch.empty(co, device=DEV)
+    kw = dict(prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV)) if prologue else {}
+    F.conv_wgrad(x.to(DEV, bf), _thin_input(gy, True), k, pad, dw, db, **kw)
+    ew = (dw.double().cpu() - wr.grad).abs().max().item()
+    eb = (db.double().cpu() - br.grad).abs().max().item()
+    assert ew <= 1e-2 * (1 + wr.grad.abs().max().item()), ew
+    assert eb <= 1e-2 * (1 + br.grad.abs().max().item()), eb
+
+
+@pytest.mark.parametrize("r", [2, 3])
+def test_wgrad_fast_shuffle_prologue(r):
+    """LDS-DMA wgrad path with a sub-pixel dy view of 32-channel planes and a prologue."""
+    g = torch.Generator().manual_seed(24)
+    bf = torch.bfloat16
+    n, h, w, ci, f = 2, 9, 21, 64, 32
+    co = f * r * r
+    x = torch.randn((n, 1, h, w, ci), generator=g)
+    sc = torch.rand(ci, generator=g) + 0.5
+    sh = torch.randn(ci, generator=g)
+    wt = torch.randn((co, ci, 3, 3), generator=g) / 24
+    gy = torch.randn((n, f, h * r, w * r), generator=g)
+    xin = torch.relu(_q(x, bf) * sc.double() + sh.double()).to(bf).double()
+    wr = _q(wt, bf).requires_grad_(True)
+    br = torch.zeros(co, dtype=torch.float64, requires_grad=True)
+    y = Fn.pixel_shuffle(Fn.conv2d(xin[:, 0].permute(0, 3, 1, 2), wr, br, padding=1), r)
+    y.backward(_q(gy, bf))
+    dw = torch.empty((co, ci, 3, 3), device=DEV)
+    db = torch.empty(co, device=DEV)
+    gy_cl = gy.permute(0, 2, 3, 1).unsqueeze(1).contiguous().to(DEV, bf)
+    F.conv_wgrad(x.to(DEV, bf), gy_cl, (1, 3, 3), (0, 1, 1), dw.view(co, ci, 1, 3, 3), db,
+                 prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV), perm_r=r, dy_shuffle=r)
+    err = (dw.double().cpu() - wr.grad).abs().max().item()
+    eb = (db.double().cpu() - br.grad).abs().max().item()
+    assert err <= 1e-2 * (1 + wr.grad.abs().max().item()), err
+    assert eb <= 1e-2 * (1 + br.grad.abs().max().item()), eb

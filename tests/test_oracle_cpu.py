@@ -48,3 +48,14 @@ def test_metrics_golden():
     for ds in ("acdc", "dsb15"):
         o, t = cpu_nets.denormalize(fx["out"], ds), cpu_nets.denormalize(fx["target"], ds)
         assert abs(cpu_nets.psnr(o, t).item() - fx[f"psnr_{ds}"]) <= 1e-5
+
+
+def test_oracle_ssim_matches_reference_fixture():
+    """The SSIM restatement (oracle/cpu_nets.ssim) against the reference's own
+    metrics.SSIM output recorded in tests/golden/metrics.pt."""
+    from oracle import cpu_nets
+    fx = load_golden("metrics")
+    for ds in ("acdc", "dsb15"):
+        o = cpu_nets.denormalize(fx["out"], ds)
+        t = cpu_nets.denormalize(fx["target"], ds)
+        assert abs(float(cpu_nets.ssim(o, t)) - fx[f"ssim_{ds}"]) <= 1e-6

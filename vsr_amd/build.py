@@ -43,14 +43,22 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     objdir = LIBDIR / "obj"
     objdir.mkdir(exist_ok=True)
 
+    headers = b"".join(p.read_bytes() for p in sorted(CSRC.glob("*.h")) + [INCLUDE / "vsrk.h"])
+
     def compile_one(src: Path) -> Path:
         obj = objdir / (src.stem + ".o")
+        # per-object stamp: recompile only when this source, a header or the flags changed
+        key = hashlib.sha256(src.read_bytes() + headers + " ".join(FLAGS).encode()).hexdigest()[:16]
+        ostamp = objdir / (src.stem + ".stamp")
+        if not force and obj.exists() and ostamp.exists() and ostamp.read_text() == key:
+            return obj
         cmd = [HIPCC, *FLAGS, "-I", str(INCLUDE), "-c", str(src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-6000:]}")
+        ostamp.write_text(key)
         return obj
 
     with ThreadPoolExecutor(max_workers=min(8, len(sources()))) as ex:

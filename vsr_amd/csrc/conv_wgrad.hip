@@ -429,7 +429,11 @@ extern "C" int vsrk_conv_wgrad(const vsrk_conv_desc* d, const vsrk_tensor5* x, c
   if (p.ntiles == 0) return VSRK_OK;
   const bool vec = a.xvec && a.dyvec;
   hipStream_t s = (hipStream_t)stream;
-  if (x->dtype == VSRK_BF16) {
+  if (x->dtype == VSRK_BF16 && vsrk_conv_wgrad_thin(a, p.nco, p.nci, perm_r, s)) {
+    // thin-channel kernel (conv_thin.hip), same slab layout
+  } else if (x->dtype == VSRK_BF16 && vec && vsrk_conv_wgrad_fast(a, p.nco, p.nci, s)) {
+    // LDS-DMA kernel (conv_wgrad_fast.hip), same slab layout
+  } else if (x->dtype == VSRK_BF16) {
     if (p.nco == 2 && p.nci == 2) wgrad_k<bf16, 2, 2>(a, vec, s);
     else if (p.nco == 2) wgrad_k<bf16, 2, 1>(a, vec, s);
     else if (p.nci == 2) wgrad_k<bf16, 1, 2>(a, vec, s);

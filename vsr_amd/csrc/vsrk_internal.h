@@ -15,3 +15,8 @@ int vsrk_channel_reduce_internal(const vsrk_tensor5* x, int mode, int perm_r, fl
 int vsrk_conv_fwd_fast(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                        const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
+// thin-channel path of vsrk_conv_fwd (conv_thin.hip): cin <= 4 or cout <= 3;
+// same return convention.
+int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                       const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
+                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);

@@ -16,7 +16,7 @@ from ._native import ACT_NONE, ACT_PRELU, ACT_RELU, PRO_AFFINE, PRO_AFFINE_RELU,
 
 __all__ = [
     "pack_weight", "conv", "conv_wgrad", "to_view", "from_view", "relu_bwd", "add",
-    "loss_fwd", "loss_bwd", "psnr", "workspace", "LOSS_KINDS",
+    "loss_fwd", "loss_bwd", "psnr", "ssim", "workspace", "LOSS_KINDS",
     "bn_stats", "bn_finalize", "bn_fold_running", "bn_relu_bwd_reduce", "bn_relu_bwd_apply",
     "duf_dynfilter_fwd", "duf_dynfilter_bwd",
     "subpixel_conv_weight", "subpixel_wgrad_fold", "prelu_wgrad", "prelu_bwd",
@@ -239,6 +239,26 @@ def psnr(out: torch.Tensor, target: torch.Tensor, mean: float = 0.0, std: float 
     N.check(lib.vsrk_psnr(o.data_ptr(), t.data_ptr(), b, per, 1 if denormalize else 0, float(mean), float(std),
                           float(max_value),
                           ps.data_ptr(), m.data_ptr(), ws.data_ptr(), nb, N.stream_ptr(o.device)), "psnr")
+    return m, ps
+
+
+def ssim(out: torch.Tensor, target: torch.Tensor, mean: float = 0.0, std: float = 1.0, value_range: float = 255.0,
+         denormalize: bool = False):
+    """2-D SSIM of (N, C, H, W) images ([denormalized] in the kernel); returns
+    (batch mean, per-sample) as device tensors."""
+    lib = _lib()
+    if out.dim() != 4:
+        raise ValueError(f"ssim: expected (N, C, H, W) images, got {tuple(out.shape)}")
+    o = out.float().contiguous()
+    t = target.float().contiguous()
+    b, c, h, w = o.shape
+    ps = torch.empty(b, dtype=torch.float32, device=o.device)
+    m = torch.empty((), dtype=torch.float32, device=o.device)
+    nb = lib.vsrk_ssim_workspace_size(b, c, h, w)
+    ws = torch.empty(nb, dtype=torch.uint8, device=o.device)
+    N.check(lib.vsrk_ssim(o.data_ptr(), t.data_ptr(), b, c, h, w, 1 if denormalize else 0, float(mean), float(std),
+                          float(value_range), ps.data_ptr(), m.data_ptr(), ws.data_ptr(), nb,
+                          N.stream_ptr(o.device)), "ssim")
     return m, ps
 
 

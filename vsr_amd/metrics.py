@@ -1,8 +1,11 @@
 """Metrics on HIP kernels, same names/arguments as src/model/metrics.py.
 
-PSNR (metrics.py:9-36) runs as one fused reduction kernel; ``psnr_denorm``
-fuses the trainer's denormalize (utils.py:1-20) into it, which is what the
-train step calls every iteration (base_trainer.py:135).
+PSNR (metrics.py:9-36) and SSIM (metrics.py:39-113) each run as one fused
+kernel plus a fixed-order final reduction; ``psnr_denorm`` / ``ssim_denorm``
+fuse the trainer's denormalize (utils.py:1-20) into them, which is what the
+train step calls every iteration (base_trainer.py:135).  CardiacPSNR /
+CardiacSSIM (metrics.py:116-165) crop the cardiac bounding box (a view) and
+reuse them.
 """
 from __future__ import annotations
 
@@ -32,3 +35,65 @@ class PSNR(nn.Module):
     def forward(self, output, target):
         m, per = F.psnr(output, target, max_value=self.max_value, denormalize=False)
         return m if self.size_average else per
+
+
+def ssim_denorm(output: torch.Tensor, target: torch.Tensor, dataset: str, size_average: bool = True) -> torch.Tensor:
+    """SSIM(denormalize(output), denormalize(target)) in one kernel (2-D window)."""
+    mean, std = DATASET_STATS[dataset]
+    m, per = F.ssim(output, target, mean, std, 255.0, denormalize=True)
+    return m if size_average else per
+
+
+class SSIM(nn.Module):
+    """metrics.py:39-113 (dim=2): Gaussian 11x11 window (sigma 1.5), valid filtering."""
+
+    def __init__(self, dim=2, channels=1, size_average=True, value_range=255):
+        super().__init__()
+        if dim not in (2, 3):
+            raise ValueError(f"Only dim=2, 3 are supported. Received dim={dim}.")
+        if dim == 3:
+            raise NotImplementedError("the HIP SSIM covers dim=2 (what every reference config uses)")
+        self.dim = dim
+        self.channels = channels
+        self.size_average = size_average
+        self.value_range = value_range
+        self.c1 = (0.01 * value_range) ** 2
+        self.c2 = (0.03 * value_range) ** 2
+
+    def forward(self, output, target):
+        m, per = F.ssim(output, target, value_range=self.value_range)
+        return m if self.size_average else per
+
+
+def _load_coordinates(path):
+    """The reference pickles {patient name: (h0, hn, w0, wn)} (metrics.py:123-125).
+    Only a JSON map is read here (no unpickling of input files)."""
+    import json
+    with open(path) as fh:
+        return {k: tuple(v) for k, v in json.load(fh).items()}
+
+
+class CardiacPSNR(nn.Module):
+    """metrics.py:116-139: PSNR inside the patient's cardiac bounding box."""
+
+    def __init__(self, coordinates_path, **kwargs):
+        super().__init__()
+        self.psnr = PSNR(**kwargs)
+        self.coordinates = _load_coordinates(coordinates_path)
+
+    def forward(self, output, target, name):
+        h0, hn, w0, wn = self.coordinates[name]
+        return self.psnr(output[..., h0:hn, w0:wn], target[..., h0:hn, w0:wn])
+
+
+class CardiacSSIM(nn.Module):
+    """metrics.py:142-165: SSIM inside the patient's cardiac bounding box."""
+
+    def __init__(self, coordinates_path, **kwargs):
+        super().__init__()
+        self.ssim = SSIM(**kwargs)
+        self.coordinates = _load_coordinates(coordinates_path)
+
+    def forward(self, output, target, name):
+        h0, hn, w0, wn = self.coordinates[name]
+        return self.ssim(output[..., h0:hn, w0:wn], target[..., h0:hn, w0:wn])
