@@ -107,6 +107,14 @@ int vsrk_conv_fwd(const vsrk_conv_desc* desc, const vsrk_tensor5* x, const void*
  * 1 = fast path when eligible.  Results agree within bf16 rounding. */
 int vsrk_conv_set_algo(int32_t mode);
 
+/* Per-path switch for A/B measurement and tests: path "fast" (bf16 LDS-DMA
+ * conv, default on), "thin" (cin <= 4 / cout <= 3 kernels incl. their weight
+ * gradient, default on), "wgrad_fast" (LDS-DMA weight gradient, default off);
+ * mode -1 = default/environment (VSRK_CONV_FAST, VSRK_CONV_THIN,
+ * VSRK_WGRAD_FAST), 0 = off, 1 = on where eligible.  Every path computes the
+ * same result as the generic kernels within bf16 rounding. */
+int vsrk_conv_set_path(const char* path, int32_t mode);
+
 /* Weight/bias gradient (autograd of nn.Conv*d.weight/.bias in loss.backward(),
  * base_trainer.py:128).  dw is fp32 in torch layout (cout, cin, kd, kh, kw);
  * `perm_r` as in vsrk_conv_pack_weight.  Deterministic: per-workgroup fp32

@@ -241,7 +241,7 @@ THIN_FWD = [
 
 
 def _thin_input(x, padded):
-    if not padded:
+    if not padded or x.shape[-1] >= 8:
         return x.to(DEV, torch.bfloat16)
     st = torch.zeros((*x.shape[:-1], 8), dtype=torch.bfloat16, device=DEV)
     st[..., :x.shape[-1]] = x.to(DEV, torch.bfloat16)
@@ -346,9 +346,67 @@ def test_wgrad_fast_shuffle_prologue(r):
     dw = torch.empty((co, ci, 3, 3), device=DEV)
     db = torch.empty(co, device=DEV)
     gy_cl = gy.permute(0, 2, 3, 1).unsqueeze(1).contiguous().to(DEV, bf)
-    F.conv_wgrad(x.to(DEV, bf), gy_cl, (1, 3, 3), (0, 1, 1), dw.view(co, ci, 1, 3, 3), db,
-                 prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV), perm_r=r, dy_shuffle=r)
+    F.set_conv_path("wgrad_fast", 1)
+    try:
+        F.conv_wgrad(x.to(DEV, bf), gy_cl, (1, 3, 3), (0, 1, 1), dw.view(co, ci, 1, 3, 3), db,
+                     prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV), perm_r=r, dy_shuffle=r)
+    finally:
+        F.set_conv_path("wgrad_fast", -1)
     err = (dw.double().cpu() - wr.grad).abs().max().item()
     eb = (db.double().cpu() - br.grad).abs().max().item()
     assert err <= 1e-2 * (1 + wr.grad.abs().max().item()), err
     assert eb <= 1e-2 * (1 + br.grad.abs().max().item()), eb
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[4] % 8 == 0 and c[5] % 8 == 0])
+def test_wgrad_fast_path(case):
+    """the LDS-DMA weight-gradient kernel (opt-in path) against fp64 autograd."""
+    n, d, h, w, ci, co, k, pad = case
+    bf = torch.bfloat16
+    g = torch.Generator().manual_seed(25)
+    x = torch.randn((n, d, h, w, ci), generator=g)
+    wt = torch.randn((co, ci, *k), generator=g) / (ci * k[0] * k[1] * k[2]) ** 0.5
+    do = d + 2 * pad[0] - k[0] + 1
+    gy = torch.randn((n, do, h, w, co), generator=g)
+    wr = _q(wt, bf).requires_grad_(True)
+    br = torch.zeros(co, dtype=torch.float64, requires_grad=True)
+    _ref_conv(_q(x, bf), wr, br, pad).backward(_q(gy, bf))
+    dw = torch.empty((co, ci, *k), device=DEV)
+    db = torch.empty(co, device=DEV)
+    F.set_conv_path("wgrad_fast", 1)
+    try:
+        F.conv_wgrad(x.to(DEV, bf), gy.to(DEV, bf), k, pad, dw, db)
+    finally:
+        F.set_conv_path("wgrad_fast", -1)
+    ew = (dw.double().cpu() - wr.grad).abs().max().item()
+    eb = (db.double().cpu() - br.grad).abs().max().item()
+    assert ew <= 1e-2 * (1 + wr.grad.abs().max().item()), ew
+    assert eb <= 1e-2 * (1 + br.grad.abs().max().item()), eb
+
+
+@pytest.mark.parametrize("case", THIN_FWD)
+def test_thin_matches_generic(case):
+    """thin-channel kernels == the generic implicit-GEMM kernels on the same bf16 operands
+    (forward, data gradient) up to accumulation order."""
+    n, d, h, w, ci, co, k, pad, padded = case
+    g = torch.Generator().manual_seed(26)
+    bf = torch.bfloat16
+    x = _thin_input(torch.randn((n, d, h, w, ci), generator=g), padded)
+    wt = (torch.randn((co, ci, *k), generator=g) / (ci * k[0] * k[1] * k[2]) ** 0.5).to(DEV)
+    b = torch.randn(co, generator=g).to(DEV)
+    do = d + 2 * pad[0] - k[0] + 1
+    gy = _thin_input(torch.randn((n, do, h, w, co), generator=g), True)
+    dpad = tuple(kk - 1 - p for kk, p in zip(k, pad))
+    outs = []
+    for mode in (1, 0):
+        F.set_conv_path("thin", mode)
+        try:
+            y = torch.empty((n, do, h, w, co), dtype=torch.float32, device=DEV)
+            F.conv(x, F.pack_weight(wt, 0, bf), y, k, pad, bias=b)
+            dx = torch.empty((n, d, h, w, ci), dtype=torch.float32, device=DEV)
+            F.conv(gy, F.pack_weight(wt, 1, bf), dx, k, dpad)
+            outs.append((y, dx))
+        finally:
+            F.set_conv_path("thin", -1)
+    for a_, b_ in zip(outs[0], outs[1]):
+        assert (a_ - b_).abs().max().item() <= 1e-4 * (1 + b_.abs().max().item())

@@ -15,7 +15,19 @@ CASES = {
     "edsr3x3": (64, 1, 128, 128, 64, 64, (1, 3, 3), (0, 1, 1)),
     "duf3x3x3": (4, 16, 128, 128, 64, 32, (3, 3, 3), (1, 1, 1)),
     "duf1x1x1": (64, 7, 128, 128, 128, 128, (1, 1, 1), (0, 0, 0)),
+    # EDSR tail conv F -> 1 at HR (thin-channel kernels: fwd = thin-out, dgrad = thin-in)
+    "tail": (64, 1, 512, 512, 64, 1, (1, 3, 3), (0, 1, 1)),
+    "head": (64, 1, 128, 128, 1, 64, (1, 3, 3), (0, 1, 1)),
 }
+
+
+def _padded(t, dt):
+    """thin (c < 8) tensors live in 8-channel storage, as in the nets."""
+    if t.shape[-1] >= 8:
+        return t.to("cuda", dt)
+    st = torch.zeros((*t.shape[:-1], 8), dtype=dt, device="cuda")
+    st[..., :t.shape[-1]] = t.to("cuda", dt)
+    return st[..., :t.shape[-1]]
 
 
 def main():
@@ -29,13 +41,21 @@ def main():
     n, d, h, w, ci, co, k, pad = CASES[args.case]
     dt = torch.bfloat16
     g = torch.Generator(device="cpu").manual_seed(0)
-    x = torch.randn((n, d, h, w, ci), generator=g).to(dev, dt)
+    x = _padded(torch.randn((n, d, h, w, ci), generator=g), dt)
     wt = (torch.randn((co, ci, *k), generator=g) * 0.05).to(dev)
     b = torch.randn(co, generator=g).to(dev)
     do = d + 2 * pad[0] - k[0] + 1
-    y = torch.empty((n, do, h, w, co), dtype=dt, device=dev)
-    res = torch.randn((n, do, h, w, co), generator=g).to(dev, dt)
-    gy = torch.randn((n, do, h, w, co), generator=g).to(dev, dt)
+    y = torch.empty((n, do, h, w, co), dtype=dt if co >= 8 else torch.float32, device=dev)
+    res = torch.randn((n, do, h, w, co), generator=g).to(dev, y.dtype)
+    gy = _padded(torch.randn((n, do, h, w, co), generator=g), dt)
+    dx = torch.empty((n, d, h, w, ci), dtype=dt if ci >= 8 else torch.float32, device=dev)
+    wp1 = F.pack_weight(wt, 1, dt)
+    dpad = tuple(kk - 1 - p for kk, p in zip(k, pad))
+    # HBM bytes of one pass over the wide side + the narrow side (thin kernels are HBM-bound)
+    esz = {torch.bfloat16: 2, torch.float32: 4}
+    nbytes = {"fwd": x.numel() // x.shape[-1] * (ci * 2) + y.numel() * esz[y.dtype],
+              "dgrad": gy.numel() // gy.shape[-1] * (co * 2) + dx.numel() * esz[dx.dtype],
+              "wgrad": x.numel() // x.shape[-1] * (ci * 2) + gy.numel() // gy.shape[-1] * (co * 2)}
     dw = torch.empty((co, ci, *k), device=dev)
     db = torch.empty(co, device=dev)
     wp = F.pack_weight(wt, 0, dt)
@@ -44,6 +64,7 @@ def main():
         "fwd": lambda: F.conv(x, wp, y, k, pad, bias=b),
         "res": lambda: F.conv(x, wp, y, k, pad, bias=b, out_scale=0.1, residual=res),
         "wgrad": lambda: F.conv_wgrad(x, gy, k, pad, dw, db),
+        "dgrad": lambda: F.conv(gy, wp1, dx, k, dpad),
     }
     for name in args.what.split(","):
         fn = cases[name]
@@ -58,7 +79,8 @@ def main():
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / args.iters
         print(f"{args.case:10s} {name:6s} {ms * 1e3:9.1f} us  {flop / ms / 1e9:8.1f} TFLOP/s  "
-              f"({flop / ms / 1e9 / 2500 * 100:.1f}% of 2.5 PF)", flush=True)
+              f"({flop / ms / 1e9 / 2500 * 100:.1f}% of 2.5 PF)  "
+              f"{nbytes.get(name, 0) / ms / 1e9:7.2f} TB/s (min HBM bytes)", flush=True)
 
 
 if __name__ == "__main__":

@@ -30,6 +30,7 @@
 // MFMA v_mfma_f32_32x32x16_bf16, operands "weights x voxels": a lane's
 // accumulator column is one voxel, its registers 4 consecutive channels.
 #include <cstdlib>
+#include <string>
 #include "conv_common.h"
 
 namespace {
@@ -631,6 +632,16 @@ int g_fast_nw = -1;  // 3x3 fast path: 8 waves x 2 rows (default) or 4 waves x 4
 extern "C" int vsrk_conv_set_algo(int32_t mode) {
   VSRK_CHECK(mode >= -1 && mode <= 1, "conv_set_algo: mode must be -1, 0 or 1");
   g_fast_mode = mode;
+  return VSRK_OK;
+}
+
+extern "C" int vsrk_conv_set_path(const char* path, int32_t mode) {
+  VSRK_CHECK(path && mode >= -1 && mode <= 1, "conv_set_path: mode must be -1, 0 or 1");
+  const std::string p(path);
+  if (p == "fast") g_fast_mode = mode;
+  else if (p == "thin") vsrk_g_thin_mode = mode;
+  else if (p == "wgrad_fast") vsrk_g_wgrad_fast_mode = mode;
+  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, thin, wgrad_fast)", path);
   return VSRK_OK;
 }
 

@@ -27,11 +27,14 @@ using namespace vsrk_conv;
 constexpr int THR = 256;         // 4 waves
 constexpr int TH = 8;            // output tile rows
 constexpr int TWT = 32;          // output tile columns (one MFMA column block per row)
-constexpr int CG = 64;           // output channels per thin-in epilogue pass
+constexpr int CG = 32;           // output channels per thin-in epilogue pass (one MFMA block)
 constexpr int OROW = CG + 4;     // floats per voxel row of the transposed thin-in output (conflict-free)
-constexpr int PATCH_MAX = 4096;  // bf16 elements of the thin-in input patch
+constexpr int PATCH_MAX = 1024;  // bf16 elements of the thin-in input patch
+constexpr int NPF = PATCH_MAX / THR;  // patch elements prefetched per thread
 constexpr int XROW = 80;         // thin-out LDS bytes per staged voxel row (32 bf16 + 16 pad)
 constexpr int UMAX = 352;        // thin-out halo voxels per tile, padded to 32 (10 x 34 = 340)
+constexpr int NLX = UMAX * 4 / THR + 1;  // thin-out 16-byte chunks staged per thread and stage (5.5 -> 6)
+constexpr int NPW = 4;           // thin wgrad: dY patch elements per thread (cout * 10 * 34 <= 1024)
 
 struct ThinArgs {
   View x, y, res, msk;
@@ -71,40 +74,36 @@ __device__ __forceinline__ float pro_el(int prologue, const float* sc, const flo
   return v;
 }
 
-// Epilogue of E consecutive output channels co..co+E-1 of voxel (nb, dz, ho, wo).
+// Epilogue of E consecutive output channels co..co+E-1 of one voxel; yo / ro /
+// mo are the element offsets of channel co in y / residual / mask (views with
+// unit channel stride).  Full 16-byte chunks go as one load/store each.
 template <typename YT, int E>
-__device__ __forceinline__ void epi_store(const ThinArgs& a, const float* acc, int nb, int dz, int ho, int wo, int co,
-                                          float aslope, float mslope) {
+__device__ __forceinline__ void epi_chunk(const ThinArgs& a, const float* acc, const float* bias_s, int64_t yo,
+                                          int64_t ro, int64_t mo, int co, float aslope, float mslope) {
   constexpr int CE = 16 / (int)sizeof(YT);
-  YT* yp = reinterpret_cast<YT*>(a.y.ptr) + view_off(a.y, nb, dz, ho, wo, co);
+  YT* yp = reinterpret_cast<YT*>(a.y.ptr) + yo;
+  const YT* rp = reinterpret_cast<const YT*>(a.res.ptr) + ro;
+  const YT* mp = reinterpret_cast<const YT*>(a.msk.ptr) + mo;
   const bool full = E == CE && a.vec && co + E <= a.cout;
   float m[E], rr[E], o[E], v[E];
   if (full) {
     if constexpr (E == CE) {
-      if (a.has_mask)
-        Chunk<YT>::unpack(*reinterpret_cast<const uint4*>(reinterpret_cast<const YT*>(a.msk.ptr) +
-                                                          view_off(a.msk, nb, dz, ho, wo, co)), m);
-      if (a.has_res)
-        Chunk<YT>::unpack(*reinterpret_cast<const uint4*>(reinterpret_cast<const YT*>(a.res.ptr) +
-                                                          view_off(a.res, nb, dz, ho, wo, co)), rr);
+      if (a.has_mask) Chunk<YT>::unpack(*reinterpret_cast<const uint4*>(mp), m);
+      if (a.has_res) Chunk<YT>::unpack(*reinterpret_cast<const uint4*>(rp), rr);
       if (a.accumulate) Chunk<YT>::unpack(*reinterpret_cast<const uint4*>(yp), o);
     }
   } else {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const bool ok = co + e < a.cout;
-      const YT* mp = reinterpret_cast<const YT*>(a.msk.ptr);
-      const YT* rp = reinterpret_cast<const YT*>(a.res.ptr);
-      const YT* op = reinterpret_cast<const YT*>(a.y.ptr);
-      m[e] = (ok && a.has_mask) ? to_f32<YT>(mp[view_off(a.msk, nb, dz, ho, wo, co + e)]) : 0.f;
-      rr[e] = (ok && a.has_res) ? to_f32<YT>(rp[view_off(a.res, nb, dz, ho, wo, co + e)]) : 0.f;
-      o[e] = (ok && a.accumulate) ? to_f32<YT>(op[view_off(a.y, nb, dz, ho, wo, co + e)]) : 0.f;
+      m[e] = (ok && a.has_mask) ? to_f32<YT>(mp[e]) : 0.f;
+      rr[e] = (ok && a.has_res) ? to_f32<YT>(rp[e]) : 0.f;
+      o[e] = (ok && a.accumulate) ? to_f32<YT>(yp[e]) : 0.f;
     }
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    const float b = (a.bias && co + e < a.cout) ? a.bias[co + e] : 0.f;
-    float t = (acc[e] + b) * a.out_scale;
+    float t = fmaf(acc[e], a.out_scale, bias_s[e]);  // (acc + bias) * out_scale
     t = act_apply(a.act, t, aslope);
     if (a.has_mask) t = mask_apply(m[e], t, mslope);
     if (a.has_res) t += rr[e];
@@ -116,8 +115,12 @@ __device__ __forceinline__ void epi_store(const ThinArgs& a, const float* acc, i
   } else {
 #pragma unroll
     for (int e = 0; e < E; ++e)
-      if (co + e < a.cout) reinterpret_cast<YT*>(a.y.ptr)[view_off(a.y, nb, dz, ho, wo, co + e)] = from_f32<YT>(v[e]);
+      if (co + e < a.cout) yp[e] = from_f32<YT>(v[e]);
   }
+}
+
+__device__ __forceinline__ int64_t corner(const View& v, int nb, int d, int h, int w) {
+  return nb * v.sn + (int64_t)d * v.sd + (int64_t)h * v.sh + (int64_t)w * v.sw;
 }
 
 // ---------------------------------------------------------------------------
@@ -127,12 +130,17 @@ __device__ __forceinline__ void epi_store(const ThinArgs& a, const float* acc, i
 // patch (cin x kd x (8+kh-1) x (32+kw-1), prologue applied, zero padded) is
 // staged into LDS as bf16; wave w owns output rows w and w+4 and gathers their
 // im2col B fragments once; A fragments (weights, every output channel) stay
-// in registers for the whole run.  Per 64-channel group the accumulators go
+// in registers for the whole run.  Per 32-channel block the accumulators go
 // through LDS transposed to voxel-major rows and all 256 threads store
-// 16-byte channel chunks.
-template <typename YT, int KS>
-__global__ __launch_bounds__(THR) void conv_thin_in_kernel(ThinArgs a) {
-  constexpr int NCBM = 8;  // up to 256 output channels
+// 16-byte channel chunks.  Every per-thread index (patch slot, epilogue chunk)
+// is fixed for the launch and precomputed as an offset from the tile corner,
+// so a tile costs one 64-bit corner per tensor.
+template <typename YT, int KS, int NCBM>
+__global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(KS * NCBM <= 2 ? 3 : 2))) void conv_thin_in_kernel(
+    ThinArgs a) {
+  constexpr int E = 16 / (int)sizeof(YT);
+  constexpr int NCH = CG / E;         // chunks per voxel and channel block
+  constexpr int NIT = 256 * NCH / THR;  // epilogue chunks per thread and block
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float* lout = reinterpret_cast<float*>(lds);                  // [256][OROW]
   bf16* patch = reinterpret_cast<bf16*>(lds + 256 * OROW * 4);  // [cin][kd][HH][WW]
@@ -176,28 +184,70 @@ __global__ __launch_bounds__(THR) void conv_thin_in_kernel(ThinArgs a) {
         }
         afr[cb][s][j] = v;
       }
+  // patch slots: offset from the tile's input corner and (dz, h, w) position
+  int p_rel[NPF], p_geo[NPF];
+#pragma unroll
+  for (int k = 0; k < NPF; ++k) {
+    const int i = tid + k * THR;
+    const int ww = i % WW;
+    int r = i / WW;
+    const int hh = r % HH;
+    r /= HH;
+    const int dzk = r % a.kd, c = r / a.kd;
+    p_rel[k] = (int)((int64_t)dzk * a.x.sd + (int64_t)hh * a.x.sh + (int64_t)ww * a.x.sw) + c;
+    p_geo[k] = i < npatch ? ((dzk << 20) | (hh << 10) | ww) : -1;
+  }
+  // epilogue chunks: voxel v = i / NCH (row v/32, column v%32), channel chunk q = i % NCH
+  int y_rel[NIT], r_rel[NIT], m_rel[NIT], e_vx[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int i = tid + k * THR, v = i / NCH, q = i % NCH;
+    const int vr = v / 32, vc = v % 32;
+    y_rel[k] = (int)(vr * a.y.sh + vc * a.y.sw) + q * E;
+    r_rel[k] = (int)(vr * a.res.sh + vc * a.res.sw) + q * E;
+    m_rel[k] = (int)(vr * a.msk.sh + vc * a.msk.sw) + q * E;
+    e_vx[k] = (vr << 8) | vc;
+  }
+  const int qe = (tid % NCH) * E;  // channel offset of every epilogue chunk within a block
 
+  // Patch staging is software-pipelined: the next tile's elements are loaded
+  // into registers while this tile computes and stores.
   const bf16* xb = reinterpret_cast<const bf16*>(a.x.ptr);
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int t0 = L * a.tiles_per_blk, t1 = min(a.ntiles, t0 + a.tiles_per_blk);
+  bf16 pv[NPF];
+  unsigned pmask = 0;
+  auto fetch = [&](int t) __attribute__((always_inline)) {
+    const TileIdx ti = tile_at(t, a.tiles_w, a.tiles_h, a.y.d);
+    const int d0 = ti.dz - a.pd, hb = ti.h0 - a.ph, wb = ti.w0 - a.pw;
+    const bf16* base = xb + corner(a.x, ti.nb, d0, hb, wb);
+    pmask = 0;
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int g = p_geo[k];
+      const int di = d0 + (g >> 20), hi = hb + ((g >> 10) & 1023), wi = wb + (g & 1023);
+      const bool ok = g >= 0 && di >= 0 && di < a.x.d && hi >= 0 && hi < a.x.h && wi >= 0 && wi < a.x.w;
+      pv[k] = *(ok ? base + p_rel[k] : xb);
+      pmask |= (ok ? 1u : 0u) << k;
+    }
+  };
+  if (t0 < t1) fetch(t0);
   for (int t = t0; t < t1; ++t) {
     const TileIdx ti = tile_at(t, a.tiles_w, a.tiles_h, a.y.d);
-    const int hb = ti.h0 - a.ph, wb = ti.w0 - a.pw;
-    for (int i = tid; i < npatch; i += THR) {
-      const int ww = i % WW;
-      int r = i / WW;
-      const int hh = r % HH;
-      r /= HH;
-      const int dzk = r % a.kd, c = r / a.kd;
-      const int di = ti.dz + dzk - a.pd, hi = hb + hh, wi = wb + ww;
-      float v = 0.f;
-      if (di >= 0 && di < a.x.d && hi >= 0 && hi < a.x.h && wi >= 0 && wi < a.x.w) {
-        v = (float)xb[view_off(a.x, ti.nb, di, hi, wi, c)];
-        if (a.prologue) v = pro_el(a.prologue, a.pro_scale, a.pro_shift, v, c);
+#pragma unroll
+    for (int k = 0; k < NPF; ++k) {
+      const int i = tid + k * THR;
+      if (p_geo[k] >= 0) {
+        float v = 0.f;
+        if ((pmask >> k) & 1) {
+          v = (float)pv[k];
+          if (a.prologue) v = pro_el(a.prologue, a.pro_scale, a.pro_shift, v, i / (a.kd * HH * WW));
+        }
+        patch[i] = (bf16)v;
       }
-      patch[i] = (bf16)v;
     }
     __syncthreads();
+    if (t + 1 < t1) fetch(t + 1);
     bf16x8 bfr[2][KS];
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
@@ -207,39 +257,48 @@ __global__ __launch_bounds__(THR) void conv_thin_in_kernel(ThinArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) bfr[rr][s][j] = boff[s][j] >= 0 ? patch[boff[s][j] + vo] : (bf16)0.f;
     }
+    const int64_t yc = corner(a.y, ti.nb, ti.dz, ti.h0, ti.w0);
+    const int64_t rc = corner(a.res, ti.nb, ti.dz, ti.h0, ti.w0);
+    const int64_t mc = corner(a.msk, ti.nb, ti.dz, ti.h0, ti.w0);
+    const int hlim = a.y.h - ti.h0, wlim = a.y.w - ti.w0;
 #pragma unroll
-    for (int cg = 0; cg < NCBM / 2; ++cg) {
-      if (cg * CG >= a.cout) break;  // uniform
+    for (int cb = 0; cb < NCBM; ++cb) {
+      if (cb >= ncb) break;  // uniform
 #pragma unroll
       for (int rr = 0; rr < 2; ++rr) {
         const int vrow = wave + 4 * rr;
+        f32x16 acc;
 #pragma unroll
-        for (int cbl = 0; cbl < 2; ++cbl) {
-          const int cb = 2 * cg + cbl;
-          if (cb >= ncb) continue;
-          f32x16 acc;
+        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+        for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[cb][s], bfr[rr][s], acc, 0, 0, 0);
+        float* dst = lout + (vrow * 32 + n) * OROW + 4 * hf;
 #pragma unroll
-          for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[cb][s], bfr[rr][s], acc, 0, 0, 0);
-          float* dst = lout + (vrow * 32 + n) * OROW + cbl * 32 + 4 * hf;
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            *reinterpret_cast<f32x4*>(dst + 8 * j) = f32x4{acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]};
-        }
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<f32x4*>(dst + 8 * j) = f32x4{acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]};
       }
       __syncthreads();
-      constexpr int E = 16 / (int)sizeof(YT);
-      constexpr int NCH = CG / E;
-      for (int i = tid; i < 256 * NCH; i += THR) {
-        const int v = i / NCH, q = i % NCH;
-        const int co = cg * CG + q * E;
-        const int ho = ti.h0 + v / 32, wo = ti.w0 + v % 32;
-        if (co >= a.cout || ho >= a.y.h || wo >= a.y.w) continue;
-        float accv[E];
+      const int co = cb * 32 + qe;
+      float bsv[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) accv[e] = lout[v * OROW + q * E + e];
-        epi_store<YT, E>(a, accv, ti.nb, ti.dz, ho, wo, co, aslope, mslope);
+      for (int e = 0; e < E; ++e) bsv[e] = (a.bias && co + e < a.cout) ? a.bias[co + e] * a.out_scale : 0.f;
+#pragma unroll
+      for (int k = 0; k < NIT; ++k) {
+        const int vr = e_vx[k] >> 8, vc = e_vx[k] & 255;
+        if (co < a.cout && vr < hlim && vc < wlim) {
+          const float* src = lout + (vr * 32 + vc) * OROW + qe;
+          float accv[E];
+#pragma unroll
+          for (int e = 0; e < E; e += 4) {
+            const f32x4 q4 = *reinterpret_cast<const f32x4*>(src + e);
+            accv[e] = q4[0];
+            accv[e + 1] = q4[1];
+            accv[e + 2] = q4[2];
+            accv[e + 3] = q4[3];
+          }
+          epi_chunk<YT, E>(a, accv, bsv, yc + y_rel[k] + cb * 32, rc + r_rel[k] + cb * 32, mc + m_rel[k] + cb * 32,
+                           co, aslope, mslope);
+        }
       }
       __syncthreads();
     }
@@ -249,43 +308,87 @@ __global__ __launch_bounds__(THR) void conv_thin_in_kernel(ThinArgs a) {
 // ---------------------------------------------------------------------------
 // thin output: M = (tap, co)
 // ---------------------------------------------------------------------------
-// Per tile and 32-channel chunk the (8+kh-1) x (32+kw-1) halo voxels are staged
+// Per tile and 32-channel chunk the (8+KK-1) x (32+KK-1) halo voxels are staged
 // in LDS (80-byte rows: conflict-free ds_read_b128) and wave w accumulates the
 // 32-voxel blocks w, w+4, w+8 of P in registers across chunks.  P then goes to
-// LDS and thread v sums its kh*kw shifted entries per output channel.
-template <typename YT>
-__global__ __launch_bounds__(THR) void conv_thin_out_kernel(ThinArgs a) {
+// LDS and thread v sums its KK*KK shifted entries per output channel.  Stages
+// (tile, chunk) are software-pipelined through registers, and every
+// per-thread index is an offset from the stage's corner fixed for the launch.
+template <typename YT, int KK>
+__global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(3))) void conv_thin_out_kernel(ThinArgs a) {
+  constexpr int HH = TH + KK - 1, WW = TWT + KK - 1;
+  constexpr int U = HH * WW, UB = (U + 31) / 32;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* xs = lds;                                          // [UMAX][XROW]
-  float* P = reinterpret_cast<float*>(lds + UMAX * XROW);  // [32][UMAX]
+  float* P = reinterpret_cast<float*>(lds + UMAX * XROW);  // [M][UMAX]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n = lane & 31, hf = lane >> 5;
-  const int HH = TH + a.kh - 1, WW = TWT + a.kw - 1;
-  const int U = HH * WW, UB = ceil_div(U, 32);
-  const int taps2 = a.kh * a.kw, M = taps2 * a.cout;
+  const int M = KK * KK * a.cout;
   const float aslope = a.act == VSRK_ACT_PRELU ? *a.act_param : 0.f;
   const float mslope = a.mask_slope ? *a.mask_slope : 0.f;
   const int mtap = n / a.cout, mco = n % a.cout;  // this lane's A row (tap, co)
   const bf16* xb = reinterpret_cast<const bf16*>(a.x.ptr);
+  const int nch = ceil_div(a.cin, 32);
+
+  // staging slots: chunk i = tid + k*THR is piece i&3 of halo voxel u = i>>2
+  int x_rel[NLX], x_geo[NLX];
+#pragma unroll
+  for (int k = 0; k < NLX; ++k) {
+    const int i = tid + k * THR, u = i >> 2, p = i & 3;
+    const int hh = u / WW, ww = u % WW;
+    x_rel[k] = (int)((int64_t)hh * a.x.sh + (int64_t)ww * a.x.sw) + 8 * p;
+    x_geo[k] = (i < UMAX * 4 && u < U) ? ((p << 16) | (hh << 8) | ww) : -1;
+  }
+  const int vr = tid / 32, vc = tid % 32;  // this thread's output voxel in the epilogue
+  const int y_rel = (int)(vr * a.y.sh + vc * a.y.sw);
+  const int r_rel = (int)(vr * a.res.sh + vc * a.res.sw);
+  const int m_rel = (int)(vr * a.msk.sh + vc * a.msk.sw);
 
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int t0 = L * a.tiles_per_blk, t1 = min(a.ntiles, t0 + a.tiles_per_blk);
-  for (int t = t0; t < t1; ++t) {
-    const TileIdx ti = tile_at(t, a.tiles_w, a.tiles_h, a.y.d);
+  const int s0 = t0 * nch, s1 = t1 * nch;
+  uint4 rv[NLX];
+  bf16x8 afn[2], afr[2];  // A fragments (weights of the stage's chunk): next / current
+  unsigned rmask = 0;
+  auto fetch = [&](int sg) __attribute__((always_inline)) {
+    const TileIdx ti = tile_at(sg / nch, a.tiles_w, a.tiles_h, a.y.d);
+    const int c0 = (sg % nch) * 32;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = c0 + 16 * s + 8 * hf;
+      afn[s] = (n < M) ? *reinterpret_cast<const bf16x8*>(a.w + ((int64_t)mtap * a.cout_pad + mco) * a.cin_pad + c)
+                       : bf16x8{};
+    }
     const int hb = ti.h0 - a.ph, wb = ti.w0 - a.pw;
-    f32x16 acc[3];
+    const bf16* base = xb + corner(a.x, ti.nb, ti.dz, hb, wb) + c0;
+    rmask = 0;
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < NLX; ++k) {
+      const int g = x_geo[k];
+      const int hi = hb + ((g >> 8) & 255), wi = wb + (g & 255), ch = c0 + 8 * (g >> 16);
+      const bool ok = g >= 0 && hi >= 0 && hi < a.x.h && wi >= 0 && wi < a.x.w && ch < a.cin;
+      rv[k] = *reinterpret_cast<const uint4*>(ok ? base + x_rel[k] : xb);
+      rmask |= (ok ? 1u : 0u) << k;
+    }
+  };
+  f32x16 acc[3];
+  if (s0 < s1) fetch(s0);
+  for (int sg = s0; sg < s1; ++sg) {
+    const int q = sg % nch;
+    if (q == 0) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
-    for (int c0 = 0; c0 < a.cin; c0 += 32) {
-      for (int i = tid; i < UMAX * 4; i += THR) {
-        const int u = i >> 2, p = i & 3;
-        const int hh = u / WW, ww = u % WW;
-        const int hi = hb + hh, wi = wb + ww, ch = c0 + 8 * p;
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NLX; ++k) {
+      const int i = tid + k * THR;
+      if (i < UMAX * 4) {
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (u < U && hi >= 0 && hi < a.x.h && wi >= 0 && wi < a.x.w && ch < a.cin) {
-          v = *reinterpret_cast<const uint4*>(xb + view_off(a.x, ti.nb, ti.dz, hi, wi, ch));
+        if ((rmask >> k) & 1) {
+          v = rv[k];
           if (a.prologue) {
+            const int ch = q * 32 + 8 * (i & 3);
             float f[8];
             Chunk<bf16>::unpack(v, f);
 #pragma unroll
@@ -293,31 +396,29 @@ __global__ __launch_bounds__(THR) void conv_thin_out_kernel(ThinArgs a) {
             v = Chunk<bf16>::pack(f);
           }
         }
-        *reinterpret_cast<uint4*>(xs + u * XROW + p * 16) = v;
+        *reinterpret_cast<uint4*>(xs + (i >> 2) * XROW + (i & 3) * 16) = v;
       }
-      __syncthreads();
-      bf16x8 afr[2];
+    }
+    afr[0] = afn[0];
+    afr[1] = afn[1];
+    __syncthreads();
+    if (sg + 1 < s1) fetch(sg + 1);
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int c = c0 + 16 * s + 8 * hf;
-        if (n < M && c < a.cin_pad)
-          afr[s] = *reinterpret_cast<const bf16x8*>(a.w + ((int64_t)mtap * a.cout_pad + mco) * a.cin_pad + c);
-        else
-          afr[s] = bf16x8{};
-      }
+    for (int i = 0; i < 3; ++i) {
+      const int ub = wave + 4 * i;
+      if (ub < UB) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int ub = wave + 4 * i;
-        if (ub < UB) {
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(xs + (ub * 32 + n) * XROW + (16 * s + 8 * hf) * 2);
-            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[s], bfr, acc[i], 0, 0, 0);
-          }
+        for (int s = 0; s < 2; ++s) {
+          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(xs + (ub * 32 + n) * XROW + (16 * s + 8 * hf) * 2);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[s], bfr, acc[i], 0, 0, 0);
         }
       }
-      __syncthreads();
     }
+    if (q + 1 < nch) {
+      __syncthreads();  // xs is restaged by the next stage
+      continue;
+    }
+    const TileIdx ti = tile_at(sg / nch, a.tiles_w, a.tiles_h, a.y.d);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int ub = wave + 4 * i;
@@ -331,21 +432,23 @@ __global__ __launch_bounds__(THR) void conv_thin_out_kernel(ThinArgs a) {
           }
       }
     }
-    __syncthreads();
-    {
-      const int vr = tid / 32, vc = tid % 32;
-      const int ho = ti.h0 + vr, wo = ti.w0 + vc;
-      if (ho < a.y.h && wo < a.y.w) {
-        for (int co = 0; co < a.cout; ++co) {
-          float s = 0.f;
-          for (int khk = 0; khk < a.kh; ++khk)
-            for (int kwk = 0; kwk < a.kw; ++kwk)
-              s += P[((khk * a.kw + kwk) * a.cout + co) * UMAX + (vr + khk) * WW + vc + kwk];
-          epi_store<YT, 1>(a, &s, ti.nb, ti.dz, ho, wo, co, aslope, mslope);
-        }
+    __syncthreads();  // P complete; every wave is done reading xs
+    if (ti.h0 + vr < a.y.h && ti.w0 + vc < a.y.w) {
+      const int64_t yo = corner(a.y, ti.nb, ti.dz, ti.h0, ti.w0) + y_rel;
+      const int64_t ro = corner(a.res, ti.nb, ti.dz, ti.h0, ti.w0) + r_rel;
+      const int64_t mo = corner(a.msk, ti.nb, ti.dz, ti.h0, ti.w0) + m_rel;
+      for (int co = 0; co < a.cout; ++co) {
+        float sum = 0.f;
+#pragma unroll
+        for (int khk = 0; khk < KK; ++khk)
+#pragma unroll
+          for (int kwk = 0; kwk < KK; ++kwk)
+            sum += P[((khk * KK + kwk) * a.cout + co) * UMAX + (vr + khk) * WW + vc + kwk];
+        const float bs = a.bias ? a.bias[co] * a.out_scale : 0.f;
+        epi_chunk<YT, 1>(a, &sum, &bs, yo + co, ro + co, mo + co, co, aslope, mslope);
       }
     }
-    __syncthreads();
+    // P is rewritten only after the next tile's first stage barrier
   }
 }
 
@@ -360,7 +463,7 @@ __global__ __launch_bounds__(THR) void conv_thin_out_kernel(ThinArgs a) {
 // Wave w runs k-steps w, w+4, w+8, w+12 (16 voxels each); the four wave
 // partials and the dbias partials are summed in a fixed order at the end.
 template <int NCI>
-__global__ __launch_bounds__(THR) void conv_wgrad_thin_kernel(WgradArgs a) {
+__global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(NCI == 1 ? 3 : 2))) void conv_wgrad_thin_kernel(WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* xs = lds;                                           // [NCI][256][64 B]
   bf16* dyp = reinterpret_cast<bf16*>(lds + NCI * 256 * 64);  // [cout][HH][WW]
@@ -388,17 +491,49 @@ __global__ __launch_bounds__(THR) void conv_wgrad_thin_kernel(WgradArgs a) {
     for (int e = 0; e < 16; ++e) acc[p][e] = 0.f;
   float bsum[3] = {0.f, 0.f, 0.f};
 
+  // Staging is software-pipelined: tile t+1's x chunks and dY patch are
+  // loaded into registers while tile t computes.
   const int t_begin = split * a.tiles_per_split;
   const int t_end = min(a.ntiles, t_begin + a.tiles_per_split);
-  for (int t = t_begin; t < t_end; ++t) {
+  const int npat = a.cout * HH * WW;
+  uint4 xr[4 * NCI];
+  bf16 yv[NPW];
+  unsigned xmask = 0, ymask = 0;
+  auto fetch = [&](int t) __attribute__((always_inline)) {
     const TileIdx ti = tile_at(t, a.tiles_w, a.tiles_h, a.dy.d);
-    for (int i = tid; i < NCI * 1024; i += THR) {
+    xmask = 0;
+    ymask = 0;
+#pragma unroll
+    for (int k = 0; k < 4 * NCI; ++k) {
+      const int i = tid + k * THR;
       const int pl = i >> 10, rem = i & 1023, v = rem >> 2, p = rem & 3;
       const int hi = ti.h0 + v / TW, wi = ti.w0 + v % TW, ch = ci0 + pl * 32 + 8 * p;
+      const bool ok = hi < a.x.h && wi < a.x.w && ch < a.cin;
+      xr[k] = *reinterpret_cast<const uint4*>(xb + (ok ? view_off(a.x, ti.nb, ti.dz, hi, wi, ch) : 0));
+      xmask |= (ok ? 1u : 0u) << k;
+    }
+#pragma unroll
+    for (int k = 0; k < NPW; ++k) {
+      const int i = tid + k * THR;
+      const int co = i / (HH * WW), rr = i % (HH * WW), hh = rr / WW, ww = rr % WW;
+      const int hd = ti.h0 + oh + hh, wd = ti.w0 + ow + ww;
+      const bool ok = i < npat && hd >= 0 && hd < a.dy.h && wd >= 0 && wd < a.dy.w;
+      yv[k] = yb[ok ? view_off(a.dy, ti.nb, ti.dz, hd, wd, co) : 0];
+      ymask |= (ok ? 1u : 0u) << k;
+    }
+  };
+  if (t_begin < t_end) fetch(t_begin);
+  for (int t = t_begin; t < t_end; ++t) {
+    const TileIdx ti = tile_at(t, a.tiles_w, a.tiles_h, a.dy.d);
+#pragma unroll
+    for (int k = 0; k < 4 * NCI; ++k) {
+      const int i = tid + k * THR;
+      const int pl = i >> 10, rem = i & 1023, v = rem >> 2, p = rem & 3;
       uint4 val = make_uint4(0, 0, 0, 0);
-      if (hi < a.x.h && wi < a.x.w && ch < a.cin) {
-        val = *reinterpret_cast<const uint4*>(xb + view_off(a.x, ti.nb, ti.dz, hi, wi, ch));
+      if ((xmask >> k) & 1) {
+        val = xr[k];
         if (a.prologue) {
+          const int ch = ci0 + pl * 32 + 8 * p;
           float f[8];
           Chunk<bf16>::unpack(val, f);
 #pragma unroll
@@ -408,14 +543,13 @@ __global__ __launch_bounds__(THR) void conv_wgrad_thin_kernel(WgradArgs a) {
       }
       *reinterpret_cast<uint4*>(xs + (pl * 256 + v) * 64 + p * 16) = val;
     }
-    for (int i = tid; i < a.cout * HH * WW; i += THR) {
-      const int co = i / (HH * WW), rr = i % (HH * WW), hh = rr / WW, ww = rr % WW;
-      const int hd = ti.h0 + oh + hh, wd = ti.w0 + ow + ww;
-      float v = 0.f;
-      if (hd >= 0 && hd < a.dy.h && wd >= 0 && wd < a.dy.w) v = (float)yb[view_off(a.dy, ti.nb, ti.dz, hd, wd, co)];
-      dyp[i] = (bf16)v;
+#pragma unroll
+    for (int k = 0; k < NPW; ++k) {
+      const int i = tid + k * THR;
+      if (i < npat) dyp[i] = ((ymask >> k) & 1) ? yv[k] : (bf16)0.f;
     }
     __syncthreads();
+    if (t + 1 < t_end) fetch(t + 1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int vb = (wave + 4 * i) * 16;
@@ -505,17 +639,18 @@ void launch_persistent(KF kern, ThinArgs& a, size_t lds, hipStream_t s) {
   kern<<<grid, THR, lds, s>>>(a);
 }
 
-int g_thin_mode = -1;  // VSRK_CONV_THIN=0 disables the thin kernels
-
-bool thin_enabled() {
-  if (g_thin_mode < 0) {
-    const char* e = getenv("VSRK_CONV_THIN");
-    g_thin_mode = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_thin_mode != 0;
-}
-
 }  // namespace
+
+int vsrk_g_thin_mode = -1;  // -1: from VSRK_CONV_THIN (default on), 0 off, 1 on (vsrk_conv_set_path)
+
+static bool thin_enabled() {
+  int m = vsrk_g_thin_mode;
+  if (m < 0) {
+    const char* e = getenv("VSRK_CONV_THIN");
+    m = (e && e[0] == '0') ? 0 : 1;
+  }
+  return m != 0;
+}
 
 // 1 = launched; 0 = not a thin conv (the implicit-GEMM kernels run); < 0 = -(error status).
 int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
@@ -568,18 +703,32 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   if (a.ntiles == 0) return 1;
   const bool yb = y->dtype == VSRK_BF16;
   if (thin_in) {
-    const size_t lds = (size_t)256 * OROW * 4 + PATCH_MAX * 2;
+    const size_t lds = (size_t)256 * OROW * 4 + PATCH_MAX * 2;  // 36.9 KB + 2 KB: 3 workgroups per CU
+    const int ncb = ceil_div(y->c, 32);
+#define VSRK_THIN_IN(KS, NCB)                                                     \
+  do {                                                                            \
+    if (yb) launch_persistent(conv_thin_in_kernel<bf16, KS, NCB>, a, lds, s);     \
+    else launch_persistent(conv_thin_in_kernel<float, KS, NCB>, a, lds, s);       \
+  } while (0)
     if (K <= 16) {
-      if (yb) launch_persistent(conv_thin_in_kernel<bf16, 1>, a, lds, s);
-      else launch_persistent(conv_thin_in_kernel<float, 1>, a, lds, s);
+      if (ncb <= 2) VSRK_THIN_IN(1, 2);
+      else if (ncb <= 4) VSRK_THIN_IN(1, 4);
+      else VSRK_THIN_IN(1, 8);
     } else {
-      if (yb) launch_persistent(conv_thin_in_kernel<bf16, 2>, a, lds, s);
-      else launch_persistent(conv_thin_in_kernel<float, 2>, a, lds, s);
+      if (ncb <= 2) VSRK_THIN_IN(2, 2);
+      else if (ncb <= 4) VSRK_THIN_IN(2, 4);
+      else VSRK_THIN_IN(2, 8);
     }
+#undef VSRK_THIN_IN
   } else {
-    const size_t lds = (size_t)UMAX * XROW + (size_t)32 * UMAX * 4;
-    if (yb) launch_persistent(conv_thin_out_kernel<bf16>, a, lds, s);
-    else launch_persistent(conv_thin_out_kernel<float>, a, lds, s);
+    const size_t lds = (size_t)UMAX * XROW + (size_t)d->kh * d->kw * y->c * UMAX * 4;
+    if (d->kh == 3) {
+      if (yb) launch_persistent(conv_thin_out_kernel<bf16, 3>, a, lds, s);
+      else launch_persistent(conv_thin_out_kernel<float, 3>, a, lds, s);
+    } else {
+      if (yb) launch_persistent(conv_thin_out_kernel<bf16, 1>, a, lds, s);
+      else launch_persistent(conv_thin_out_kernel<float, 1>, a, lds, s);
+    }
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -596,6 +745,7 @@ int vsrk_conv_wgrad_thin(const vsrk_conv::WgradArgs& a, int nco, int nci, int pe
   if (nco != 1 || a.cout > 3 || a.kd != 1 || a.pd != 0 || a.kh != a.kw || a.kh * a.kw * a.cout > 32) return 0;
   if (a.cin % 8 || !a.xvec || a.x.r > 1 || a.dy.r > 1 || perm_r > 1) return 0;
   if (a.x.h != a.dy.h || a.x.w != a.dy.w || a.x.d != a.dy.d) return 0;
+  if (a.cout * (GTH + a.kh - 1) * (TW + a.kw - 1) > NPW * THR) return 0;
   const size_t stage = (size_t)nci * 256 * 64 + (size_t)a.cout * (GTH + a.kh - 1) * (TW + a.kw - 1) * 2;
   const size_t lds = std::max(stage, (size_t)4 * nci * 1024 * 4);
   if (nci == 2) {

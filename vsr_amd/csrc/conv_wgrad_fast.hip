@@ -374,11 +374,15 @@ bool wgrad_fast_k(const WgradArgs& a, hipStream_t s) {
 // 1 = launched; 0 = not eligible (the generic kernel runs).  Needs bf16
 // chunk-readable views (checked by the caller), kh = kw in {1, 3}, channel
 // counts in whole 16-byte chunks and sub-pixel planes of whole 32-channel rows.
+int vsrk_g_wgrad_fast_mode = -1;  // -1: from VSRK_WGRAD_FAST (default off), 0 off, 1 on (vsrk_conv_set_path)
+
 int vsrk_conv_wgrad_fast(const vsrk_conv::WgradArgs& a, int nco, int nci, hipStream_t s) {
-  static int mode = -1;
+  int mode = vsrk_g_wgrad_fast_mode;
   if (mode < 0) {
+    // opt-in: at one workgroup of 4 waves per CU it trails conv_wgrad_kernel
+    // (2 workgroups per CU) on the EDSR 64->64 shape
     const char* e = getenv("VSRK_WGRAD_FAST");
-    mode = (e && e[0] == '0') ? 0 : 1;
+    mode = (e && e[0] == '1') ? 1 : 0;
   }
   if (!mode) return 0;
   if (a.kh != a.kw || (a.kh != 1 && a.kh != 3)) return 0;

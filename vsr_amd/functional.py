@@ -154,6 +154,11 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, k, pad, dw: torch.Tensor, dbia
     N.check(rc, "conv_wgrad")
 
 
+def set_conv_path(path: str, mode: int) -> None:
+    """Select a conv kernel family ("fast", "thin", "wgrad_fast"): -1 default, 0 off, 1 on."""
+    N.check(_lib().vsrk_conv_set_path(path.encode(), int(mode)), "conv_set_path")
+
+
 def to_view(src: torch.Tensor, dtype: torch.dtype, cpad: int | None = None) -> torch.Tensor:
     """(N, C, [D,] H, W) fp32 -> channels-last (N, D, H, W, cpad) in dtype (zero padded).
     Slice [..., :C] of a padded result for a C-channel view the kernels can
