@@ -7,6 +7,7 @@ raised (the product path never silently drops to a PyTorch/CPU op).
 from __future__ import annotations
 
 import ctypes as C
+import os
 import threading
 from pathlib import Path
 
@@ -94,7 +95,9 @@ _lock = threading.Lock()
 
 
 def lib_path() -> Path:
-    return _build.LIB
+    # VSRK_LIB: an alternative build of the same ABI (A/B kernel experiments)
+    alt = os.environ.get("VSRK_LIB")
+    return Path(alt) if alt else _build.LIB
 
 
 def load(build_if_missing: bool = False):

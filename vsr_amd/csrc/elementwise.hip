@@ -46,6 +46,28 @@ __global__ void ncdhw_to_view_kernel(const float* __restrict__ src, int n, int c
   reinterpret_cast<T*>(dst.ptr)[view_off(dst, nn, dd, hh, ww, ch)] = from_f32<T>(v);
 }
 
+// Dense channels-last destination (the network edges: the LR input and the HR
+// output gradient in their zero-padded 8-channel storage).  One thread per
+// voxel writes whole 16-byte chunks (padding channels as zeros); the only
+// division is voxel -> (sample, spatial offset).  The generic kernel above
+// spends its time in the 64-bit div/mod chain of decode_voxel per element.
+template <typename T>
+__global__ void ncdhw_to_dense_kernel(const float* __restrict__ src, int c, int dhw, int cp, int nvox,
+                                      T* __restrict__ dst) {
+  constexpr int E = Chunk<T>::E;
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= nvox) return;
+  const int nn = v / dhw, rem = v - nn * dhw;
+  const float* s = src + (int64_t)nn * c * dhw + rem;
+  uint4* o = reinterpret_cast<uint4*>(dst + (int64_t)v * cp);
+  for (int c0 = 0; c0 < cp; c0 += E) {
+    float f[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) f[e] = (c0 + e < c) ? __builtin_nontemporal_load(s + (int64_t)(c0 + e) * dhw) : 0.f;
+    o[c0 / E] = Chunk<T>::pack(f);
+  }
+}
+
 template <typename T>
 __global__ void view_to_ncdhw_kernel(View src, float* __restrict__ dst, int c, int64_t total) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -262,6 +284,20 @@ extern "C" int vsrk_ncdhw_to_view(const float* src, int32_t n, int32_t c, int32_
   View v = make_view(dst);
   const int64_t total = nvox(dst) * dst->c;
   hipStream_t s = (hipStream_t)stream;
+  const int64_t cp = dst->c, dhw = (int64_t)d * h * w;
+  const int esz = dst->dtype == VSRK_BF16 ? 2 : 4;
+  const bool dense = dst->shuffle <= 1 && dst->sw == cp && dst->sh == w * cp && dst->sd == h * dst->sh &&
+                     dst->sn == d * dst->sd && (cp * esz) % 16 == 0 && ((uintptr_t)dst->ptr) % 16 == 0 &&
+                     nvox(dst) < (1ll << 31) && dhw * c < (1ll << 31);
+  if (dense) {
+    const int nv = (int)nvox(dst);
+    if (dst->dtype == VSRK_BF16)
+      ncdhw_to_dense_kernel<bf16><<<ceil_div(nv, 256), 256, 0, s>>>(src, c, (int)dhw, (int)cp, nv, (bf16*)dst->ptr);
+    else
+      ncdhw_to_dense_kernel<float><<<ceil_div(nv, 256), 256, 0, s>>>(src, c, (int)dhw, (int)cp, nv, (float*)dst->ptr);
+    VSRK_LAUNCH_CHECK("ncdhw_to_view(dense)");
+    return VSRK_OK;
+  }
   if (dst->dtype == VSRK_BF16)
     ncdhw_to_view_kernel<bf16><<<(int)ceil_div64(total, 256), 256, 0, s>>>(src, n, c, d, h, w, v, total);
   else
