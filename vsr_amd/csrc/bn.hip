@@ -17,29 +17,36 @@ namespace {
 
 constexpr int RB = 512;  // reduction blocks (partials)
 
-__device__ __forceinline__ void decode_voxel(int64_t v, const View& t, int& n, int& d, int& h, int& w) {
-  w = v % t.w;
-  v /= t.w;
-  h = v % t.h;
-  v /= t.h;
-  d = v % t.d;
-  n = v / t.d;
+// Row decomposition: a "row" is one (n, d, h) line of W voxels.  Threads are
+// (voxel lane vl, chunk position ch) with ch fixed for the launch, so a
+// thread's per-channel constants live in registers; the (n, d, h) decode is
+// 32-bit and once per row, and consecutive lanes read consecutive 16-byte
+// chunks of a voxel row (coalesced for dense tensors and channel slices of
+// the DUF concat buffer alike).  The first version decoded every voxel with a
+// 64-bit div/mod chain and re-read the per-channel tables per element: the
+// BN+ReLU backward apply took 8.5 ms per launch at the DUF cfg-2 shapes.
+__device__ __forceinline__ int64_t row_off(const View& v, int r) {
+  const int h = r % v.h, t = r / v.h;
+  const int d = t % v.d, n = t / v.d;
+  return n * v.sn + (int64_t)d * v.sd + (int64_t)h * v.sh;
 }
 
 // modes: 0 = sum x, sum x^2 (stats); 1 = sum dy, sum dy*xhat with
-// dy = dz * (x*scale + shift > 0) (BN+ReLU backward)
+// dy = dz * (x*scale + shift > 0) (BN+ReLU backward).  Block b reduces rows
+// [b*rpb, (b+1)*rpb) into partial b (fixed order: deterministic).
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void chan_reduce_kernel(View x, View dz, const float* __restrict__ scale,
                                                           const float* __restrict__ shift,
                                                           const float* __restrict__ mean,
-                                                          const float* __restrict__ invstd, int64_t nvox,
+                                                          const float* __restrict__ invstd, int nrows, int rpb,
                                                           float* __restrict__ part) {
   constexpr int E = Chunk<T>::E;
   const int C = x.c;
   const int cpv = (C + E - 1) / E;  // chunks per voxel
-  const int vpb = blockDim.x / cpv; // voxels per block iteration (blockDim is a multiple of cpv)
+  const int vpb = blockDim.x / cpv; // voxel lanes (blockDim is a multiple of cpv)
   const int ch = threadIdx.x % cpv, vl = threadIdx.x / cpv;
   const int c0 = ch * E;
+  const bool full = c0 + E <= C;
   float s1[E], s2[E], sc[E], sh[E], mu[E], is[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
@@ -54,39 +61,40 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(View x, View dz, const
     }
   }
   if (vl < vpb) {
-    const int64_t per = (nvox + gridDim.x - 1) / gridDim.x;
-    const int64_t v0 = blockIdx.x * per, v1 = min(nvox, v0 + per);
-    for (int64_t v = v0 + vl; v < v1; v += vpb) {
-      int n, d, h, w;
-      decode_voxel(v, x, n, d, h, w);
-      float f[E];
-      const T* px = reinterpret_cast<const T*>(x.ptr) + view_off(x, n, d, h, w, c0);
-      if (c0 + E <= C) {
-        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(px), f);
-      } else {
-#pragma unroll
-        for (int e = 0; e < E; ++e) f[e] = c0 + e < C ? to_f32<T>(px[e]) : 0.f;
-      }
-      if (MODE == 0) {
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          s1[e] += f[e];
-          s2[e] = fmaf(f[e], f[e], s2[e]);
-        }
-      } else {
-        float g[E];
-        const T* pg = reinterpret_cast<const T*>(dz.ptr) + view_off(dz, n, d, h, w, c0);
-        if (c0 + E <= C) {
-          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(pg), g);
+    const int r0 = blockIdx.x * rpb, r1 = min(nrows, r0 + rpb);
+    for (int r = r0; r < r1; ++r) {
+      const T* xr = reinterpret_cast<const T*>(x.ptr) + row_off(x, r) + c0;
+      const T* gr = MODE == 1 ? reinterpret_cast<const T*>(dz.ptr) + row_off(dz, r) + c0 : nullptr;
+      for (int w = vl; w < x.w; w += vpb) {
+        float f[E];
+        const T* px = xr + (int64_t)w * x.sw;
+        if (full) {
+          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(px), f);
         } else {
 #pragma unroll
-          for (int e = 0; e < E; ++e) g[e] = c0 + e < C ? to_f32<T>(pg[e]) : 0.f;
+          for (int e = 0; e < E; ++e) f[e] = c0 + e < C ? to_f32<T>(px[e]) : 0.f;
         }
+        if (MODE == 0) {
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const float dy = fmaf(f[e], sc[e], sh[e]) > 0.f ? g[e] : 0.f;
-          s1[e] += dy;
-          s2[e] = fmaf(dy, (f[e] - mu[e]) * is[e], s2[e]);
+          for (int e = 0; e < E; ++e) {
+            s1[e] += f[e];
+            s2[e] = fmaf(f[e], f[e], s2[e]);
+          }
+        } else {
+          float g[E];
+          const T* pg = gr + (int64_t)w * dz.sw;
+          if (full) {
+            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(pg), g);
+          } else {
+#pragma unroll
+            for (int e = 0; e < E; ++e) g[e] = c0 + e < C ? to_f32<T>(pg[e]) : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const float dy = fmaf(f[e], sc[e], sh[e]) > 0.f ? g[e] : 0.f;
+            s1[e] += dy;
+            s2[e] = fmaf(dy, (f[e] - mu[e]) * is[e], s2[e]);
+          }
         }
       }
     }
@@ -114,17 +122,33 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(View x, View dz, const
   }
 }
 
-__global__ void chan_final_kernel(const float* __restrict__ part, int nblk, int C, float* __restrict__ o1,
-                                  float* __restrict__ o2) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// One block per channel: each thread sums a strided subset of the partials in
+// double, then a fixed-shape tree (deterministic).  The first version ran one
+// thread per channel over all partials serially (133 us per call, 26 calls
+// per DUF step).
+__global__ __launch_bounds__(256) void chan_final_kernel(const float* __restrict__ part, int nblk, int C,
+                                                         float* __restrict__ o1, float* __restrict__ o2) {
+  const int c = blockIdx.x, t = threadIdx.x;
   double a = 0.0, b = 0.0;
-  for (int k = 0; k < nblk; ++k) {
+  for (int k = t; k < nblk; k += 256) {
     a += part[((int64_t)k * 2) * C + c];
     b += part[((int64_t)k * 2 + 1) * C + c];
   }
-  o1[c] = (float)a;
-  o2[c] = (float)b;
+  __shared__ double ra[256], rb[256];
+  ra[t] = a;
+  rb[t] = b;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) {
+      ra[t] += ra[t + off];
+      rb[t] += rb[t + off];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    o1[c] = (float)ra[0];
+    o2[c] = (float)rb[0];
+  }
 }
 
 __global__ void bn_finalize_kernel(const float* __restrict__ sum, const float* __restrict__ sumsq, double count,
@@ -162,7 +186,8 @@ __global__ void bn_fold_running_kernel(const float* __restrict__ gamma, const fl
   shift[c] = b - rmean[c] * g * is;
 }
 
-// dx [+]= gamma*invstd*(dy - sum_dy/M - xhat*sum_dy_xhat/M), dy = dz*(x*scale+shift > 0)
+// dx [+]= gamma*invstd*(dy - sum_dy/M - xhat*sum_dy_xhat/M), dy = dz*(x*scale+shift > 0),
+// folded per channel into dx = k1*dy + k2*x + k3 (constants in registers).
 template <typename T>
 __global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(View x, View dz, View dx,
                                                                 const float* __restrict__ scale,
@@ -172,51 +197,63 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(View x, View dz,
                                                                 const float* __restrict__ gamma,
                                                                 const float* __restrict__ sdy,
                                                                 const float* __restrict__ sdyx, float inv_count,
-                                                                int64_t nchunks, int accumulate) {
+                                                                int nrows, int accumulate) {
   constexpr int E = Chunk<T>::E;
   const int C = x.c;
   const int cpv = (C + E - 1) / E;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nchunks;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int ch = i % cpv;
-    const int64_t v = i / cpv;
-    int n, d, h, w;
-    decode_voxel(v, x, n, d, h, w);
-    const int c0 = ch * E;
-    const bool full = c0 + E <= C;
-    float f[E], g[E], o[E];
-    const T* px = reinterpret_cast<const T*>(x.ptr) + view_off(x, n, d, h, w, c0);
-    const T* pg = reinterpret_cast<const T*>(dz.ptr) + view_off(dz, n, d, h, w, c0);
-    T* po = reinterpret_cast<T*>(dx.ptr) + view_off(dx, n, d, h, w, c0);
-    if (full) {
-      Chunk<T>::unpack(*reinterpret_cast<const uint4*>(px), f);
-      Chunk<T>::unpack(*reinterpret_cast<const uint4*>(pg), g);
-      if (accumulate) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(po), o);
-    } else {
+  const int vpb = blockDim.x / cpv;
+  const int ch = threadIdx.x % cpv, vl = threadIdx.x / cpv;
+  if (vl >= vpb) return;
+  const int c0 = ch * E;
+  const bool full = c0 + E <= C;
+  float sc[E], sh[E], k1[E], k2[E], k3[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int c = min(c0 + e, C - 1);
+    const float is = invstd[c], gm = gamma ? gamma[c] : 1.f;
+    const float a = gm * is, b = is * sdyx[c] * inv_count;
+    sc[e] = scale[c];
+    sh[e] = shift[c];
+    k1[e] = a;
+    k2[e] = -a * b;
+    k3[e] = a * (mean[c] * b - sdy[c] * inv_count);
+  }
+  for (int r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const T* xr = reinterpret_cast<const T*>(x.ptr) + row_off(x, r) + c0;
+    const T* gr = reinterpret_cast<const T*>(dz.ptr) + row_off(dz, r) + c0;
+    T* orow = reinterpret_cast<T*>(dx.ptr) + row_off(dx, r) + c0;
+    for (int w = vl; w < x.w; w += vpb) {
+      const T* px = xr + (int64_t)w * x.sw;
+      const T* pg = gr + (int64_t)w * dz.sw;
+      T* po = orow + (int64_t)w * dx.sw;
+      float f[E], g[E], o[E];
+      if (full) {
+        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(px), f);
+        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(pg), g);
+        if (accumulate) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(po), o);
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const bool ok = c0 + e < C;
+          f[e] = ok ? to_f32<T>(px[e]) : 0.f;
+          g[e] = ok ? to_f32<T>(pg[e]) : 0.f;
+          o[e] = (ok && accumulate) ? to_f32<T>(po[e]) : 0.f;
+        }
+      }
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const bool ok = c0 + e < C;
-        f[e] = ok ? to_f32<T>(px[e]) : 0.f;
-        g[e] = ok ? to_f32<T>(pg[e]) : 0.f;
-        o[e] = (ok && accumulate) ? to_f32<T>(po[e]) : 0.f;
+        const float dy = fmaf(f[e], sc[e], sh[e]) > 0.f ? g[e] : 0.f;
+        float rr = fmaf(k1[e], dy, fmaf(k2[e], f[e], k3[e]));
+        if (accumulate) rr += o[e];
+        o[e] = rr;
       }
-    }
+      if (full) {
+        *reinterpret_cast<uint4*>(po) = Chunk<T>::pack(o);
+      } else {
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int c = min(c0 + e, C - 1);
-      const float dy = fmaf(f[e], scale[c], shift[c]) > 0.f ? g[e] : 0.f;
-      const float xh = (f[e] - mean[c]) * invstd[c];
-      const float gm = gamma ? gamma[c] : 1.f;
-      float r = gm * invstd[c] * (dy - sdy[c] * inv_count - xh * sdyx[c] * inv_count);
-      if (accumulate) r += o[e];
-      o[e] = r;
-    }
-    if (full) {
-      *reinterpret_cast<uint4*>(po) = Chunk<T>::pack(o);
-    } else {
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-        if (c0 + e < C) po[e] = from_f32<T>(o[e]);
+        for (int e = 0; e < E; ++e)
+          if (c0 + e < C) po[e] = from_f32<T>(o[e]);
+      }
     }
   }
 }
@@ -228,23 +265,29 @@ int reduce_launch(int mode, const vsrk_tensor5* x, const vsrk_tensor5* dz, const
   const int cpv = ceil_div(x->c, E);
   VSRK_CHECK(cpv <= 256, "bn: too many channels (%d)", x->c);
   const int vpb = 256 / cpv;
-  const int64_t nv = (int64_t)x->n * x->d * x->h * x->w;
-  const int nblk = (int)std::min<int64_t>(RB, std::max<int64_t>(1, ceil_div64(nv, 64)));
+  const int64_t nr64 = (int64_t)x->n * x->d * x->h;
+  VSRK_CHECK(nr64 < (1ll << 31), "bn: too many rows");
+  const int nrows = (int)nr64;
+  const int rpb = std::max(1, ceil_div(nrows, RB));
+  const int nblk = std::max(1, ceil_div(nrows, rpb));
   const size_t need = (size_t)nblk * 2 * x->c * sizeof(float);
   VSRK_CHECK(ws && ws_bytes >= need, "bn: workspace %zu < %zu bytes", ws_bytes, need);
+  VSRK_CHECK(x->shuffle <= 1 && (!dz || (dz->shuffle <= 1 && dz->n == x->n && dz->d == x->d && dz->h == x->h &&
+                                         dz->w == x->w)),
+             "bn: sub-pixel views / mismatched x, dz shapes are not supported");
   View vx = make_view(x);
   View vg = dz ? make_view(dz) : vx;
   float* part = (float*)ws;
   const int thr = cpv * vpb;
   if (x->dtype == VSRK_BF16) {
-    if (mode == 0) chan_reduce_kernel<bf16, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nv, part);
-    else chan_reduce_kernel<bf16, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nv, part);
+    if (mode == 0) chan_reduce_kernel<bf16, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
+    else chan_reduce_kernel<bf16, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
   } else {
-    if (mode == 0) chan_reduce_kernel<float, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nv, part);
-    else chan_reduce_kernel<float, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nv, part);
+    if (mode == 0) chan_reduce_kernel<float, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
+    else chan_reduce_kernel<float, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
   }
   VSRK_LAUNCH_CHECK("bn_reduce");
-  chan_final_kernel<<<ceil_div(x->c, 256), 256, 0, s>>>(part, nblk, x->c, o1, o2);
+  chan_final_kernel<<<x->c, 256, 0, s>>>(part, nblk, x->c, o1, o2);
   VSRK_LAUNCH_CHECK("bn_reduce_final");
   return VSRK_OK;
 }
@@ -298,17 +341,26 @@ extern "C" int vsrk_bn_relu_bwd_apply(const vsrk_tensor5* x, const vsrk_tensor5*
   VSRK_CHECK(x->dtype == dz->dtype && x->dtype == dx->dtype && x->c == dz->c && x->c == dx->c,
              "bn_relu_bwd_apply: view mismatch");
   const int E = x->dtype == VSRK_BF16 ? 8 : 4;
-  const int64_t nchunks = (int64_t)x->n * x->d * x->h * x->w * ceil_div(x->c, E);
-  const int grid = (int)std::min<int64_t>(8192, ceil_div64(nchunks, 256));
+  const int cpv = ceil_div(x->c, E);
+  VSRK_CHECK(cpv <= 256, "bn_relu_bwd_apply: too many channels (%d)", x->c);
+  VSRK_CHECK(dz->n == x->n && dz->d == x->d && dz->h == x->h && dz->w == x->w && dx->n == x->n &&
+                 dx->d == x->d && dx->h == x->h && dx->w == x->w && x->shuffle <= 1 && dz->shuffle <= 1 &&
+                 dx->shuffle <= 1,
+             "bn_relu_bwd_apply: view shape mismatch");
+  const int64_t nr64 = (int64_t)x->n * x->d * x->h;
+  VSRK_CHECK(nr64 < (1ll << 31), "bn_relu_bwd_apply: too many rows");
+  const int nrows = (int)nr64;
+  const int thr = cpv * (256 / cpv);
+  const int grid = std::min(nrows, 4096);
   hipStream_t s = (hipStream_t)stream;
   if (x->dtype == VSRK_BF16)
-    bn_relu_bwd_apply_kernel<bf16><<<grid, 256, 0, s>>>(make_view(x), make_view(dz), make_view(dx), scale, shift,
+    bn_relu_bwd_apply_kernel<bf16><<<grid, thr, 0, s>>>(make_view(x), make_view(dz), make_view(dx), scale, shift,
                                                         mean, invstd, gamma, sum_dy, sum_dy_xhat,
-                                                        (float)(1.0 / count), nchunks, accumulate);
+                                                        (float)(1.0 / count), nrows, accumulate);
   else
-    bn_relu_bwd_apply_kernel<float><<<grid, 256, 0, s>>>(make_view(x), make_view(dz), make_view(dx), scale, shift,
+    bn_relu_bwd_apply_kernel<float><<<grid, thr, 0, s>>>(make_view(x), make_view(dz), make_view(dx), scale, shift,
                                                          mean, invstd, gamma, sum_dy, sum_dy_xhat,
-                                                         (float)(1.0 / count), nchunks, accumulate);
+                                                         (float)(1.0 / count), nrows, accumulate);
   VSRK_LAUNCH_CHECK("bn_relu_bwd_apply");
   return VSRK_OK;
 }
