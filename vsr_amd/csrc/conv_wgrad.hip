@@ -1,5 +1,6 @@
 // Implicit-GEMM convolution weight/bias gradient on CDNA4 MFMA (gfx950).
 // Design notes: conv_fwd.hip (layout) and the comment block below.
+#include <cstdlib>
 #include "conv_common.h"
 
 namespace {
@@ -351,7 +352,20 @@ static WgradPlan wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, cons
   p.n_ci_chunks = ceil_div(x->c, 32 * p.nci);
   p.ncombos = p.n_co_tiles * p.n_ci_chunks * d->kd;
   p.ntiles = dy->n * dy->d * ceil_div(dy->h, GTH) * ceil_div(dy->w, TW);
-  int want = ceil_div(512, p.ncombos);  // ~2 rounds of one workgroup per CU
+  // Splits (workgroups per combo): about 512 workgroups (two resident per
+  // CU), but no fewer than 16 tiles (of 8x32 voxels) per workgroup while that
+  // still leaves one workgroup per CU: each workgroup writes a whole fp32 slab
+  // and the reduce reads it back, which at 8 tiles per workgroup cost the
+  // EDSR 64->64 wgrad 10 % (147 -> 133 us at 256 workgroups; DUF's 3x3x3,
+  // at 24 tiles per workgroup, keeps its 512: 231 vs 324 us at 256).
+  // VSRK_WGRAD_TARGET=<workgroups> overrides the rule (A/B only).
+  static int target = -1;
+  if (target < 0) {
+    const char* e = getenv("VSRK_WGRAD_TARGET");
+    target = e ? std::max(64, atoi(e)) : 0;
+  }
+  int want = target ? ceil_div(target, p.ncombos)
+                    : std::min(ceil_div(512, p.ncombos), std::max(ceil_div(p.ntiles, 16), ceil_div(256, p.ncombos)));
   want = std::max(1, std::min(want, p.ntiles));
   p.tps = ceil_div(p.ntiles, want);
   p.nsplit = ceil_div(p.ntiles, p.tps);
