@@ -1,28 +1,43 @@
 #!/usr/bin/env python
 """Throughput benchmark of the cardiac cine-MRI SR train step on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--model edsr|duf|drf]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--models edsr,duf]
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver, N > 1)
+
+With --gpus N > 1 and no torchrun environment, bench.py starts the N ranks
+itself (one process per GPU, before any GPU call); under torchrun --gpus must
+equal WORLD_SIZE.
 
 A step is one full train step (generator forward, L1 loss, backward, Adam)
 over one synthetic batch of the BASELINE cfg-2 shape: per GPU a 4 x 16 x
-128 x 128 cine volume at 4x SR (bf16).  Each rank holds its own volume
-(weak scaling: data-parallel, gradients all-reduced over RCCL).
+128 x 128 cine volume at 4x SR.  Each rank holds its own volume (weak
+scaling: data-parallel, gradients all-reduced over RCCL, BatchNorm statistics
+synchronised for DUF).
+
+Models (each timed on its own, all reported in the one JSON line):
+  edsr  EDSRNet on the volume's 64 slices (2-D residual blocks + PixelShuffle)
+  duf   DUFNet on the volume's 64 seven-frame cyclic windows (Conv3d 3x3x3 /
+        BatchNorm3d dense blocks + dynamic upsampling filter)
+The top-level value/roofline are the first model's; "models" holds each one.
 
 metric  = LR voxels/s (one LR input voxel of a target frame; B*T*H*W =
           1,048,576 per GPU per step), whole job.
-roofline: the dominant kernel's algorithmic FLOP per launch / its mean
-          launch time (HIP events on the launch stream, inside the timed
-          region) against the 2.5 PFLOP/s dense bf16 MFMA peak.
+roofline: the model's dominant conv, forward + data gradient + weight
+          gradient together: algorithmic FLOP (2*cin*cout*taps per output
+          voxel, three times) over the summed launch time of those kernels
+          (HIP events on the launch stream, inside the timed region), against
+          the dense MFMA peak of the compute dtype.  EDSR: the 33 body convs
+          3x3 64->64; DUF: the six Conv3d 3x3x3 F->32 (F = 64..224).
 cpu_baseline: the CPU fp32 restatement of the same generator (oracle/,
           the reference's algorithm) timed on this host for a bounded sample
-          (rank 0, N = 1 only).
+          (rank 0, N = 1 only), threads = the CPU share of this process.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 from pathlib import Path
@@ -36,12 +51,11 @@ sys.path.insert(0, str(ROOT))
 from vsr_amd import _native, nets  # noqa: E402
 from vsr_amd import functional as F  # noqa: E402
 from vsr_amd.data import cyclic_windows, synth_cine  # noqa: E402
-from vsr_amd.ddp import GradSync  # noqa: E402
+from vsr_amd.ddp import GradSync, enable_sync_bn  # noqa: E402
 from vsr_amd.losses import L1Loss  # noqa: E402
 
 METRIC = "voxels/sec fwd+bwd, 4× SR on 16×128×128 cine volumes, 1/2/4/8 MI355X"
-PEAK_BF16 = 2.5e15
-PEAK_F32 = 157.3e12
+PEAK = {"bf16": 2.5e15, "fp16": 2.5e15, "fp32": 157.3e12}
 B, T, H, W, R = 4, 16, 128, 128, 4
 
 MODELS = {
@@ -64,52 +78,80 @@ def make_batch(task, lr, hr):
     return [lr[:, t:t + 1] for t in range(T)], [hr[:, t:t + 1] for t in range(T)]
 
 
+def _vox(v) -> int:
+    return v.n * v.d * v.h * v.w
+
+
 def dominant(model):
-    """(kernel selector, algorithmic FLOP per launch, description)."""
+    """(matcher, description).  matcher(kind, xv, yv) -> algorithmic FLOP of the
+    launch (counted as the forward conv's 2*cin*cout*taps per forward output
+    voxel) when it is one of the roofline kernels, else 0.  xv/yv are the
+    launch's logical views (for the weight gradient: input and output grad)."""
     if model == "edsr":
-        n = B * T
-        flop = 2 * 64 * 64 * 9 * n * H * W
+        def match(kind, xv, yv):
+            if kind[1] != (1, 3, 3) or xv.c != 64 or yv.c != 64 or xv.h != H or yv.h != H:
+                return 0
+            if xv.shuffle > 1 or yv.shuffle > 1:
+                return 0
+            return 2 * 64 * 64 * 9 * _vox(yv)  # fwd: y is the output; dgrad: same size; wgrad: yv = dy
 
-        def match(kind, x, y):
-            return kind == ("conv_fwd", (1, 3, 3)) and x.shape[-1] == 64 and y.shape[-1] == 64 and y.shape[2] == H
-
-        return match, flop, f"conv3x3 64->64 bf16 implicit-GEMM (fwd+dgrad launches), {n}x{H}x{W} per launch"
+        return match, (f"EDSR body conv3x3 64->64 bf16 implicit-GEMM, fwd + dgrad + wgrad per layer, "
+                       f"{B * T}x{H}x{W} per launch (33 layers)")
     if model == "duf":
-        n = B * T
+        def match(kind, xv, yv):
+            if kind[1] != (3, 3, 3):
+                return 0
+            if kind[0] == "conv_wgrad" and yv.c == 32:  # x: unit input (F ch), dy: unit output grad
+                return 2 * 27 * xv.c * 32 * _vox(yv)
+            if kind[0] == "conv_fwd" and yv.c == 32:  # forward: y = unit output
+                return 2 * 27 * xv.c * 32 * _vox(yv)
+            if kind[0] == "conv_fwd" and xv.c == 32:  # data gradient: x = dy (forward output)
+                return 2 * 27 * yv.c * 32 * _vox(xv)
+            return 0
 
-        def match(kind, x, y):
-            return kind == ("conv_fwd", (3, 3, 3)) and x.shape[-1] == 64 and y.shape[-1] == 32
+        return match, (f"DUF Conv3d 3x3x3 F->32 (F = 64..224) bf16 implicit-GEMM, fwd + dgrad + wgrad, "
+                       f"{B * T} windows x 7 x {H}x{W}")
 
-        flop = 2 * 32 * 64 * 27 * n * 7 * H * W
-        return match, flop, f"conv3d 3x3x3 64->32 bf16 implicit-GEMM, {n}x7x{H}x{W} per launch"
-    n = B
+    def match(kind, xv, yv):
+        # LR (128^2, 64 ch) -> HR sub-pixel store: the up projection's forward and
+        # the down projection's data gradient; reference FLOP of ConvTranspose2d
+        # 64->64 8x8/4: 64*(8/4)^2 MACs per HR output value (the 3x3 sub-pixel
+        # form executes 2.25x that)
+        if kind == ("conv_fwd", (1, 3, 3)) and xv.c == 64 and xv.h == H and yv.shuffle == R:
+            return 2 * 64 * 64 * 4 * xv.n * (R * H) * (R * W)
+        return 0
 
-    def match(kind, x, y):
-        # LR (128^2, 64 ch) -> HR sub-pixel store: the up projection's forward
-        # and the down projection's data gradient (same shape)
-        return kind == ("conv_fwd", (1, 3, 3)) and x.shape[-1] == 64 and x.shape[2] == H and y.shape[2] == R * H
-
-    # the reference's algorithmic FLOP: ConvTranspose2d(64, 64, 8, stride 4),
-    # 64*(8/4)^2 MACs per HR output value (the 3x3 sub-pixel form executes 2.25x that)
-    flop = 2 * 64 * 64 * 4 * n * (R * H) * (R * W)
-    return match, flop, f"DRF 4x up projection (ConvTranspose2d 64->64 8x8/4 as sub-pixel 3x3 conv), {n}x{H}x{W} LR per launch"
+    return match, "DRF 4x up projection (ConvTranspose2d 64->64 8x8/4 as sub-pixel 3x3 conv)"
 
 
 def _traffic(model, precision):
-    """HBM bytes per launch of the dominant kernel, from the committed
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench
+    """HBM bytes per launch of the model's forward roofline kernel, from the
+    committed rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench
     (tools/pmc_traffic.py, gfx950 FETCH_SIZE correction applied), or None."""
     p = ROOT / "profiles" / f"traffic_{model}_{precision}.json"
     if not p.exists():
-        return None
-    return json.loads(p.read_text())["traffic_bytes"]
+        return None, None
+    d = json.loads(p.read_text())
+    return d["traffic_bytes"], d.get("kernel")
+
+
+def cpu_threads() -> int:
+    """Threads for the CPU baseline: this process's CPU share (OMP_NUM_THREADS
+    where the box sets it to the share, else the CPUs this process may run on)."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def cpu_baseline(model, budget_s=20.0):
     """Reference algorithm (oracle CPU restatement) on this host, bounded sample."""
     from oracle import cpu_nets
 
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     torch.set_num_threads(threads)
     spec = MODELS[model]
     cls = {"EDSRNet": cpu_nets.EDSRRef, "DUFNet": cpu_nets.DUFRef, "DRFNet": cpu_nets.DRFRef}[spec["cls"]]
@@ -154,40 +196,15 @@ def cpu_baseline(model, budget_s=20.0):
             "sample": f"{sample}; median of {len(times)} steps after 1 warm-up ({med:.2f} s/step)"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", default=os.environ.get("VSR_BENCH_MODEL", "edsr"), choices=list(MODELS))
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # VSR_BENCH_BACKEND=gloo rehearses the N>1 path (GradSync, max-over-ranks
-    # timing) with every rank on the GPUs one box has; the measured path is
-    # RCCL ("nccl"), one process per GPU.
-    backend = os.environ.get("VSR_BENCH_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % max(1, torch.cuda.device_count())
-    if world > 1:
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    _native.load()
-
-    spec = MODELS[args.model]
+def run_model(name, args, world, rank, dev):
+    spec = MODELS[name]
     torch.manual_seed(0)  # identical initial weights on every rank
     net = getattr(nets, spec["cls"])(**spec["kwargs"]).to(dev).set_precision(args.precision).train()
     opt = torch.optim.Adam(net.parameters(), lr=1e-4)
-    sync = GradSync(net, world) if world > 1 else None
+    sync = None
+    if world > 1:
+        sync = GradSync(net, world)
+        enable_sync_bn(net)  # DUF's BatchNorm3d: global-batch statistics (SyncBN)
     lr, hr = synth_cine(B, T, H, W, R, seed=1234 + rank, device=dev)
     x, y = make_batch(spec["task"], lr, hr)
     l1 = L1Loss()
@@ -207,7 +224,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    match, flop_launch, kdesc = dominant(args.model)
+    match, kdesc = dominant(name)
     F.timer = F.KernelTimer(match)
     if world > 1:
         dist.barrier()
@@ -219,35 +236,113 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = F.timer.mean_ms()
+    flop, kernel_s, launches = F.timer.totals()
     F.timer = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     vox_step = B * T * H * W
-    value = world * vox_step * args.steps / elapsed
-    peak = PEAK_BF16 if args.precision == "bf16" else PEAK_F32
-    achieved = flop_launch / (kernel_ms * 1e-3) if kernel_ms == kernel_ms else None  # NaN: no launch matched
+    peak = PEAK[args.precision]
+    achieved = flop / kernel_s if kernel_s > 0 else None
+    traffic, tkern = _traffic(name, args.precision)
+    res = {
+        "value": world * vox_step * args.steps / elapsed, "unit": "voxels/s",
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "config": {"workload": f"cfg2: ACDC 4x SR, {B}x{T}x{H}x{W} LR cine volume per GPU, "
+                               f"{spec['cls']} ({spec['task'].upper()}), L1 + Adam",
+                   "model": spec["cls"], "global_batch": world * B * T, "seq_len": T,
+                   "parallelism": f"dp{world}" + ("+syncbn" if world > 1 and name == "duf" else "")},
+        "roofline": {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None, "peak": peak / 1e12,
+                     "unit": "TFLOP/s", "frac": achieved / peak if achieved else None, "traffic": traffic,
+                     "traffic_kernel": tkern, "kernel": kdesc,
+                     "kernel_ms_per_step": kernel_s / args.steps * 1e3, "launches_per_step": launches / args.steps,
+                     "flop_per_step": flop / args.steps},
+        "final_loss": float(loss.item()),
+    }
+    del net, opt, sync
+    torch.cuda.empty_cache()
+    return res
+
+
+def worker(args, world, rank, local):
+    backend = os.environ.get("VSR_BENCH_BACKEND", "nccl")
+    # VSR_BENCH_BACKEND=gloo rehearses the N>1 path with every rank on the GPUs
+    # one box has; the measured path is RCCL ("nccl"), one process per GPU.
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
+    if world > 1:
+        torch.cuda.set_device(local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    _native.load()
+
+    names = [m for m in args.models.split(",") if m]
+    results = {m: run_model(m, args, world, rank, dev) for m in names}
     if rank == 0:
-        res = {
-            "metric": METRIC, "value": value, "unit": "voxels/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        first = results[names[0]]
+        out = {
+            "metric": METRIC, "value": first["value"], "unit": "voxels/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": first["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
-            "config": {"workload": f"cfg2: ACDC 4x SR, {B}x{T}x{H}x{W} LR cine volume per GPU, "
-                                   f"{spec['cls']} ({spec['task'].upper()}), L1 + Adam",
-                       "model": spec["cls"], "global_batch": world * B * T, "seq_len": T,
-                       "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None, "peak": peak / 1e12,
-                         "unit": "TFLOP/s", "frac": achieved / peak if achieved else None, "traffic": _traffic(args.model, args.precision), "kernel": kdesc,
-                         "kernel_ms": kernel_ms if achieved else None, "flop_per_launch": flop_launch},
-            "final_loss": float(loss.item()),
+            "config": first["config"], "roofline": first["roofline"], "final_loss": first["final_loss"],
+            "models": results,
         }
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(args.model)
-        print(json.dumps(res), flush=True)
+            for m in names:
+                results[m]["cpu_baseline"] = cpu_baseline(m)
+            out["cpu_baseline"] = results[names[0]]["cpu_baseline"]
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _spawned(local, args, world, port):
+    os.environ.update(RANK=str(local), LOCAL_RANK=str(local), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    worker(args, world, local, local)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--models", default=os.environ.get("VSR_BENCH_MODELS", "edsr,duf"),
+                    help="comma-separated subset of " + ",".join(MODELS))
+    ap.add_argument("--model", default=None, help="a single model (same as --models NAME)")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    if args.model:
+        args.models = args.model
+    for m in args.models.split(","):
+        if m not in MODELS:
+            ap.error(f"unknown model {m!r}")
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        world = int(env_world)
+        if world != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world}", file=sys.stderr)
+            sys.exit(2)
+        worker(args, world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")))
+    elif args.gpus > 1:
+        # start the ranks here, before this process touches the GPU
+        import torch.multiprocessing as mp
+        mp.spawn(_spawned, args=(args, args.gpus, _free_port()), nprocs=args.gpus, join=True)
+    else:
+        worker(args, 1, 0, 0)
 
 
 if __name__ == "__main__":

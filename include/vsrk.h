@@ -115,6 +115,15 @@ int vsrk_conv_set_algo(int32_t mode);
  * same result as the generic kernels within bf16 rounding. */
 int vsrk_conv_set_path(const char* path, int32_t mode);
 
+/* Test knob: cap the persistent conv grids (forward / data-gradient kernels)
+ * and the weight-gradient split at max_workgroups (0 = default: one
+ * workgroup per CU and the split rule).  With a small cap a small shape runs
+ * many tiles per workgroup, i.e. the same cross-tile pipeline (DMA ring,
+ * deferred epilogue, next-tile prefetch) as the full-size shapes.  Results
+ * are identical for every cap (the weight-gradient sums are re-associated
+ * over a different split, so they agree within fp32 rounding). */
+int vsrk_conv_set_grid_cap(int32_t max_workgroups);
+
 /* Weight/bias gradient (autograd of nn.Conv*d.weight/.bias in loss.backward(),
  * base_trainer.py:128).  dw is fp32 in torch layout (cout, cin, kd, kh, kw);
  * `perm_r` as in vsrk_conv_pack_weight.  Deterministic: per-workgroup fp32

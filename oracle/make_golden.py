@@ -13,6 +13,7 @@ gradient tensors; loadable with torch.load(weights_only=True)).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 from pathlib import Path
 
@@ -43,6 +44,14 @@ CASES = {
     "drf_x4_canon": ("src.model.nets.drf_net", "DRFNet", cpu_nets.DRFRef,
                      dict(in_channels=1, out_channels=1, num_features=64, num_groups=4, upscale_factor=4),
                      "vsr", (1, 3, 1, 8, 12)),
+    # well-conditioned small cases (seed searched, see find_seed): fp32 held to 1e-4 everywhere
+    "duf_x4_cond": ("src.model.nets.duf_net", "DUFNet", cpu_nets.DUFRef,
+                    dict(in_channels=1, out_channels=1, num_frames=7, size_filter=5, upscale_factor=4,
+                         backbone="_DenseLayer16"),
+                    "misr", (1, 7, 1, 6, 8)),
+    "drf_x4_cond": ("src.model.nets.drf_net", "DRFNet", cpu_nets.DRFRef,
+                    dict(in_channels=1, out_channels=1, num_features=64, num_groups=4, upscale_factor=4),
+                    "vsr", (1, 2, 1, 4, 6)),
     "drf_sisr_x2_small": ("src.model.nets.drf_sisr_net", "DRFSISRNet", cpu_nets.DRFSISRRef,
                           dict(in_channels=1, out_channels=1, num_steps=2, num_features=16, num_groups=2,
                                upscale_factor=2),
@@ -57,6 +66,29 @@ FULL_GRAD_MAX = 20000
 # 256..1700-term fp32 dot product; draws per case
 NOISE_EPS = 2e-6
 NOISE_DRAWS = 8
+# well-conditioned fixtures (SEARCH): the seed is chosen so that no ReLU /
+# PReLU input is within MARGIN * rms of zero, and the reference's own fp32
+# gradients are then asserted within COND_MAX rel-L2 of fp64 everywhere
+MARGIN = 1e-5
+COND_MAX = 5e-5
+# their envelope's injected noise: 5e-7 of the rms per layer output and input
+# gradient, several times the measured per-layer fp32 error of these dot
+# products (2e-6 accumulated over DUF's 20+ layers exceeds the margin)
+NOISE_EPS_COND = 5e-7
+SEARCH = {"duf_x4_cond", "drf_x4_cond"}
+# fixed random directions: large gradients are pinned by their projections
+PROJ = 16
+ADAM = dict(lr=1e-3, betas=(0.9, 0.999), eps=1e-8)
+
+
+def proj(t, key, n):
+    """<t, p_i> for n seeded N(0,1) directions p_i of t's shape (the seed is a
+    digest of the parameter name, so a test regenerates the same directions)."""
+    seed = int.from_bytes(hashlib.sha256(key.encode()).digest()[:4], "little")
+    g = torch.Generator().manual_seed(seed)
+    flat = t.detach().double().flatten().cpu()
+    return torch.stack([torch.dot(flat, torch.randn(flat.numel(), generator=g, dtype=torch.float64))
+                        for _ in range(n)])
 
 
 def _inputs(kind, shape, r, g):
@@ -90,7 +122,7 @@ def _psnr(out, target, dataset="acdc"):
     return cpu_nets.psnr(cpu_nets.denormalize(out, dataset), cpu_nets.denormalize(target, dataset))
 
 
-def _bf16_envelope(cls, kwargs, lr64, hr64, g64, ref32_err, draws=4):
+def _bf16_envelope(cls, kwargs, lr64, hr64, g64, ref32_err, seed, draws=4):
     """Gradient error of an ideal bf16-storage implementation: fp64 math with
     bf16 conv weights and every conv / BatchNorm output, its input gradient
     and the network input rounded to bf16 (dithered so each draw rounds
@@ -98,7 +130,7 @@ def _bf16_envelope(cls, kwargs, lr64, hr64, g64, ref32_err, draws=4):
     bound of the HIP path is a multiple of this."""
     env = {k: (0.0 if v is not None else None) for k, v in ref32_err.items()}
     for draw in range(draws):
-        g = torch.Generator().manual_seed(SEED + 100 + draw)
+        g = torch.Generator().manual_seed(seed + 100 + draw)
 
         def q(t):
             d = t + t.abs() * 2.0 ** -12 * torch.randn(t.shape, generator=g, dtype=t.dtype)
@@ -110,7 +142,7 @@ def _bf16_envelope(cls, kwargs, lr64, hr64, g64, ref32_err, draws=4):
                 out.register_hook(q)
             return out
 
-        torch.manual_seed(SEED)
+        torch.manual_seed(seed)
         m = cls(**kwargs).double().train()
         with torch.no_grad():
             for mod in m.modules():
@@ -127,10 +159,48 @@ def _bf16_envelope(cls, kwargs, lr64, hr64, g64, ref32_err, draws=4):
     return env
 
 
-def run_case(name, spec):
+def margin(spec, seed):
+    """min over every ReLU / PReLU input x of |x| / rms(x) in an fp64 forward of
+    the restatement at `seed` (net init; inputs from seed + 1)."""
+    _, _, cls, kwargs, kind, shape = spec
+    g = torch.Generator().manual_seed(seed + 1)
+    lr, _ = _inputs(kind, shape, kwargs["upscale_factor"], g)
+    lr64 = [x.double() for x in lr] if isinstance(lr, list) else lr.double()
+    torch.manual_seed(seed)
+    m = cls(**kwargs).double().train()
+    worst = [float("inf")]
+
+    def hook(mod, inp, out):
+        x = inp[0].detach()
+        worst[0] = min(worst[0], (x.abs().min() / x.pow(2).mean().sqrt()).item())
+
+    for mod in m.modules():
+        if isinstance(mod, (torch.nn.ReLU, torch.nn.PReLU)):
+            mod.register_forward_hook(hook)
+    with torch.no_grad():
+        m(lr64)
+    return worst[0]
+
+
+def find_seed(name, spec, start=SEED, tries=80):
+    """First seed (net init and inputs) at which no ReLU / PReLU input lies
+    within MARGIN * rms of zero.  fp32 rounding (a few 1e-7..1e-6 of the rms
+    for these dot products) then cannot flip any activation mask, so every
+    gradient is well-conditioned and the fixture holds an fp32 implementation
+    to SURVEY §8d's 1e-4 rel-L2 on every parameter."""
+    for seed in range(start, start + tries):
+        m = margin(spec, seed)
+        if m >= MARGIN:
+            print(f"  {name}: seed {seed}, activation margin {m:.2e} rms", flush=True)
+            return seed
+    raise SystemExit(f"{name}: no seed in [{start}, {start + tries}) with activation margin >= {MARGIN}")
+
+
+def run_case(name, spec, seed=SEED):
     modname, clsname, mine_cls, kwargs, kind, shape = spec
     ref_cls = getattr(ref_loader.load(modname), clsname)
     r = kwargs["upscale_factor"]
+    SEED = seed  # noqa: N806 (the case's seed: net init and, +1, inputs)
     torch.manual_seed(SEED)
     ref = ref_cls(**kwargs)
     torch.manual_seed(SEED)
@@ -201,9 +271,10 @@ def run_case(name, spec):
     noise_err = {k: (0.0 if v is not None else None) for k, v in ref32_err.items()}
     gn = torch.Generator().manual_seed(SEED + 7)
 
+    eps = NOISE_EPS_COND if name in SEARCH else NOISE_EPS
+
     def _jitter(t):
-        return t + NOISE_EPS * t.detach().pow(2).mean().sqrt() * torch.randn(t.shape, generator=gn,
-                                                                              dtype=t.dtype)
+        return t + eps * t.detach().pow(2).mean().sqrt() * torch.randn(t.shape, generator=gn, dtype=t.dtype)
 
     def _hook(mod, inp, out):
         out = _jitter(out)
@@ -222,7 +293,29 @@ def run_case(name, spec):
             if noise_err[k] is not None:
                 noise_err[k] = max(noise_err[k], (p.grad - g64[k]).norm().item() / g64[k].norm().item())
     ref32_err = {k: (None if v is None else max(v, noise_err[k])) for k, v in ref32_err.items()}
-    bf16_env = _bf16_envelope(mine_cls, kwargs, lr64, hr64, g64, ref32_err)
+    bf16_env = _bf16_envelope(mine_cls, kwargs, lr64, hr64, g64, ref32_err, SEED)
+    worst = max(v for v in ref32_err.values() if v is not None)
+    if name in SEARCH:
+        assert worst <= COND_MAX, f"{name}: seed {SEED} is not well-conditioned ({worst:.1e} > {COND_MAX})"
+    # projections of every fp64 gradient on fixed random directions (seeded
+    # per parameter): pins large gradients that are not stored in full.  For a
+    # Gaussian direction p, E[<e, p>^2] = |e|^2, so the rms of the projected
+    # error over PROJ directions estimates the rel-L2 error.
+    proj64 = {k: proj(v, k, PROJ) for k, v in g64.items()}
+    # one Adam step (main.py:73) from the reference's fp32 gradients
+    torch.manual_seed(SEED)
+    ma = mine_cls(**kwargs).train()
+    _loss(ma(lr), hr).backward()
+    opt = torch.optim.Adam(ma.parameters(), **ADAM)
+    p0 = {k: p.detach().clone() for k, p in ma.named_parameters()}
+    opt.step()
+    adam_update = {k: (p.detach() - p0[k]) for k, p in ma.named_parameters()}
+    # eval mode after the train step (BatchNorm from the updated running stats;
+    # base_trainer.py:130-134 validation)
+    mine.eval()
+    with torch.no_grad():
+        out_eval = mine(lr)
+    mine.train()
     fx = {
         "name": name, "class": clsname, "kwargs": kwargs, "seed": SEED, "kind": kind,
         "param_sum": init_sum,
@@ -242,11 +335,18 @@ def run_case(name, spec):
         "noise_err": noise_err,
         "bf16_env": bf16_env,
         "grad_max64": gmax,
+        "grad_proj64": proj64, "proj_n": PROJ,
+        "adam": {**ADAM, "betas": list(ADAM["betas"])},
+        "adam_update_full": {k: v for k, v in adam_update.items() if v.numel() <= FULL_GRAD_MAX},
+        "adam_update_proj": {k: proj(v.double(), k, PROJ) for k, v in adam_update.items()},
+        "adam_update_norm": {k: v.double().norm().item() for k, v in adam_update.items()},
+        "output_eval": [o.detach() for o in out_eval] if isinstance(out_eval, list) else out_eval.detach(),
+        "cond_worst": worst,
+        "act_margin": margin(spec, SEED),
     }
     OUT.mkdir(parents=True, exist_ok=True)
     torch.save(fx, OUT / f"{name}.pt")
     size = os.path.getsize(OUT / f"{name}.pt")
-    worst = max(v for v in ref32_err.values() if v is not None)
     print(f"{name}: restatement == reference (bitwise), loss={fx['loss_l1']:.6f} psnr={fx['psnr_acdc']:.4f} "
           f"fp32-vs-fp64: out {out_err32:.1e}, worst grad {worst:.1e}; fixture {size / 1024:.0f} KiB")
 
@@ -285,8 +385,12 @@ def main():
     if not ref_loader.available():
         raise SystemExit("reference not available (build container only)")
     torch.set_num_threads(min(8, os.cpu_count() or 1))
+    only = os.environ.get("GOLDEN_ONLY")
     for name, spec in CASES.items():
-        run_case(name, spec)
+        if only and name not in only.split(","):
+            continue
+        seed = find_seed(name, spec) if name in SEARCH else SEED
+        run_case(name, spec, seed)
     run_metrics()
 
 

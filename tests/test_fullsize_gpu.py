@@ -1,0 +1,169 @@
+"""Parity at the size the bench runs (BASELINE cfg 2: a 4 x 16 x 128 x 128 LR
+cine volume, i.e. 64 slices / 64 seven-frame windows), where every conv grid
+is one workgroup per CU with thousands of tiles and the weight gradient runs
+its full-size split plan.
+
+Kernel level (bf16, the bench precision), against fp64 on the CPU:
+  * forward and data gradient: every sample is computed, three are compared
+    (a conv is per-sample independent);
+  * weight gradient: the output gradient is zero outside three samples, so
+    the fp64 reference needs only those while the kernel still walks the
+    whole grid and split plan.
+Tolerances as tests/test_conv_kernels_gpu.py (inputs rounded to bf16 before
+the fp64 reference: max |d| <= 1.5e-2 max|ref|; weight gradient 1e-2).
+
+Net level: one full train step of EDSRNet and DUFNet at the bench shape
+through the HIP path (bf16) against the oracle restatement (oracle/cpu_nets,
+the reference's algorithm, bitwise-pinned to it) run in fp32 on the same
+device with the same weights and inputs: output max |d| <= 3e-2 and mean
+<= 3e-3 (SURVEY §8d bf16 bound), PSNR within 0.01 dB, parameter gradients
+within the bf16 storage envelope (rel-L2 <= 0.1 per parameter, median <= 3e-2).
+"""
+import pytest
+import torch
+import torch.nn.functional as Fn
+
+from oracle import cpu_nets
+from vsr_amd import functional as F
+from vsr_amd import nets
+from vsr_amd.data import cyclic_windows, synth_cine
+from vsr_amd.metrics import psnr_denorm
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+PICK = [0, 33, 63]
+
+
+def _ref_conv(x_cl, w, b, pad):
+    y = Fn.conv3d(x_cl.permute(0, 4, 1, 2, 3), w, b, padding=pad)
+    return y.permute(0, 2, 3, 4, 1)
+
+
+def _tol(ref):
+    return 1.5e-2 * max(ref.abs().max().item(), 1e-3)
+
+
+# (name, N, D, H, W, Cin, Cout, k, pad, prologue)
+CASES = [
+    ("edsr_body_64x64", 64, 1, 128, 128, 64, 64, (1, 3, 3), (0, 1, 1), None),
+    ("duf_conv3d_64_pad1", 64, 7, 128, 128, 64, 32, (3, 3, 3), (1, 1, 1), "bn"),
+    ("duf_conv3d_160_valid", 64, 7, 128, 128, 160, 32, (3, 3, 3), (0, 1, 1), "bn"),
+    ("duf_filter_1x1x1_256_512", 64, 1, 128, 128, 256, 512, (1, 1, 1), (0, 0, 0), "relu"),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_fullsize_conv(case):
+    name, n, d, h, w, ci, co, k, pad, pro = case
+    torch.manual_seed(11)
+    x = torch.randn((n, d, h, w, ci), device=DEV).to(BF)
+    wt = torch.randn((co, ci, *k), device=DEV) / (ci * k[0] * k[1] * k[2]) ** 0.5
+    b = torch.randn(co, device=DEV)
+    sc = torch.rand(ci, device=DEV) + 0.5
+    sh = torch.randn(ci, device=DEV)
+    do = d + 2 * pad[0] - k[0] + 1
+    res = torch.randn((n, do, h, w, co), device=DEV).to(BF)
+    kw = {}
+    if pro == "bn":
+        kw = dict(prologue=F.PRO_AFFINE_RELU, pro_scale=sc, pro_shift=sh)
+    elif pro == "relu":
+        kw = dict(prologue=F.PRO_RELU)
+
+    def prologue64(xs):
+        xs = xs.double()
+        if pro == "bn":
+            return torch.relu(xs * sc.double().cpu() + sh.double().cpu()).to(BF).double()
+        if pro == "relu":
+            return torch.relu(xs)
+        return xs
+
+    w64 = wt.cpu().to(BF).double()
+    # forward (residual + out_scale epilogue, as the EDSR res-block's second conv)
+    y = torch.empty((n, do, h, w, co), dtype=BF, device=DEV)
+    F.conv(x, F.pack_weight(wt, 0, BF), y, k, pad, bias=b, out_scale=0.1, residual=res, **kw)
+    torch.cuda.synchronize()
+    for i in PICK:
+        ref = _ref_conv(prologue64(x[i:i + 1].cpu()), w64, b.cpu().double(), pad) * 0.1 + res[i:i + 1].cpu().double()
+        err = (y[i:i + 1].cpu().double() - ref).abs().max().item()
+        assert err <= _tol(ref), (name, "fwd", i, err)
+    del y
+    # data gradient (ReLU-mask epilogue, as a dgrad through an activation)
+    gy = torch.randn((n, do, h, w, co), device=DEV).to(BF)
+    mask = torch.randn((n, d, h, w, ci), device=DEV).to(BF)
+    dpad = tuple(kk - 1 - p for kk, p in zip(k, pad))
+    dx = torch.empty((n, d, h, w, ci), dtype=BF, device=DEV)
+    F.conv(gy, F.pack_weight(wt, 1, BF), dx, k, dpad, mask=mask)
+    torch.cuda.synchronize()
+    for i in PICK:
+        xr = torch.zeros((1, d, h, w, ci), dtype=torch.float64, requires_grad=True)
+        _ref_conv(xr, w64, None, pad).backward(gy[i:i + 1].cpu().double())
+        ref = torch.where(mask[i:i + 1].cpu().double() > 0, xr.grad, torch.zeros_like(xr.grad))
+        err = (dx[i:i + 1].cpu().double() - ref).abs().max().item()
+        assert err <= _tol(ref), (name, "dgrad", i, err)
+    del dx, mask
+    # weight gradient: dy zero outside PICK
+    keep = torch.zeros(n, device=DEV)
+    keep[PICK] = 1
+    gz = (gy.float() * keep.view(n, 1, 1, 1, 1)).to(BF)
+    dw = torch.empty((co, ci, *k), dtype=torch.float32, device=DEV)
+    db = torch.empty(co, dtype=torch.float32, device=DEV)
+    F.conv_wgrad(x, gz, k, pad, dw, db, **kw)
+    torch.cuda.synchronize()
+    wr = torch.zeros((co, ci, *k), dtype=torch.float64, requires_grad=True)
+    br = torch.zeros(co, dtype=torch.float64, requires_grad=True)
+    xs = prologue64(x[PICK].cpu())
+    _ref_conv(xs, wr, br, pad).backward(gz[PICK].cpu().double())
+    ew = (dw.cpu().double() - wr.grad).abs().max().item()
+    eb = (db.cpu().double() - br.grad).abs().max().item()
+    assert ew <= 1e-2 * (1 + wr.grad.abs().max().item()), (name, "wgrad", ew)
+    assert eb <= 1e-2 * (1 + br.grad.abs().max().item()), (name, "bgrad", eb)
+
+
+def _flat_grads(net):
+    return {k: p.grad.detach().float() for k, p in net.named_parameters() if p.grad is not None}
+
+
+@pytest.mark.parametrize("model", ["edsr", "duf"])
+def test_fullsize_train_step_vs_oracle(model):
+    B, T, H, W, R = 4, 16, 128, 128, 4
+    lr, hr = synth_cine(B, T, H, W, R, seed=1234, device=DEV)
+    if model == "edsr":
+        kwargs = dict(in_channels=1, out_channels=1, num_resblocks=16, num_features=64, upscale_factor=R)
+        mine_cls, ref_cls = nets.EDSRNet, cpu_nets.EDSRRef
+        x, y = lr.reshape(B * T, 1, H, W), hr.reshape(B * T, 1, H * R, W * R)
+    else:
+        kwargs = dict(in_channels=1, out_channels=1, num_frames=7, size_filter=5, upscale_factor=R,
+                      backbone="_DenseLayer16")
+        mine_cls, ref_cls = nets.DUFNet, cpu_nets.DUFRef
+        x, y = cyclic_windows(lr, 7), hr.reshape(B * T, 1, H * R, W * R)
+    torch.manual_seed(0)
+    mine = mine_cls(**kwargs).to(DEV).set_precision("bf16").train()
+    torch.manual_seed(0)
+    ref = ref_cls(**kwargs).to(DEV).train()
+    ref.load_state_dict(mine.state_dict())
+    out = mine(x)
+    Fn.l1_loss(out, y).backward()
+    with torch.backends.cudnn.flags(enabled=False):  # the oracle through plain im2col + GEMM, fp32
+        rout = ref(x)
+        Fn.l1_loss(rout, y).backward()
+    torch.cuda.synchronize()
+    d = (out.detach() - rout.detach()).abs()
+    assert d.max().item() <= 3e-2 and d.mean().item() <= 3e-3, (d.max().item(), d.mean().item())
+    assert abs(psnr_denorm(out.detach(), y, "acdc").item() - psnr_denorm(rout.detach(), y, "acdc").item()) <= 0.01
+    g_m, g_r = _flat_grads(mine), _flat_grads(ref)
+    rels = {}
+    gmax = max(v.norm().item() for v in g_r.values())
+    for k, gr in g_r.items():
+        if gr.norm().item() <= 1e-6 * gmax:  # exact gradient ~0 (conv bias before a BatchNorm)
+            assert g_m[k].norm().item() <= 2e-2 * gmax, k
+            continue
+        rels[k] = (g_m[k] - gr).norm().item() / gr.norm().item()
+    worst = max(rels.items(), key=lambda kv: kv[1])
+    med = sorted(rels.values())[len(rels) // 2]
+    assert worst[1] <= 0.1 and med <= 3e-2, (worst, med)
+    if model == "duf":  # BatchNorm running statistics after the step
+        for k, v in ref.state_dict().items():
+            if "running" in k:
+                got = mine.state_dict()[k]
+                assert (got - v).abs().max().item() <= 2e-2 * (1 + v.abs().max().item()), k

@@ -31,7 +31,25 @@ bf16 HIP path: output max |d| <= 3e-2, mean |d| <= 3e-3; gradient rel-L2 <=
   well-conditioned parameters and ~25% on DUF's BatchNorm parameters and
   EDSR's final bias; zero-gradient parameters <= 2e-2 * max norm.
 PSNR within 0.01 dB of the reference's fp32 PSNR for both.
+
+Well-conditioned fixtures (duf_x4_cond, drf_x4_cond; oracle/make_golden.py
+find_seed): the seed is chosen so that no ReLU / PReLU input lies within
+1e-5 * rms of zero, so no fp32 rounding can flip an activation mask and the
+reference's own fp32 gradients sit within 2e-5 of fp64.  There the fp32 HIP
+path is held to SURVEY §8d's 1e-4 rel-L2 on EVERY parameter, with no
+envelope term.
+
+Gradients stored in full (<= 20000 elements) are compared element-wise;
+larger ones through 16 fixed random projections of the fp64 gradient
+(rms of the projected error estimates the rel-L2 error; a wrong gradient
+with the right norm cannot pass).
+
+Also: the eval-mode forward after the step (BatchNorm from the updated
+running statistics, the validation step base_trainer.py:130-134) and one
+Adam step (main.py:73) on the HIP gradients against the reference's update.
 """
+import hashlib
+
 import pytest
 import torch
 
@@ -77,7 +95,27 @@ def _psnr(out, hr):
 
 
 CASES = ["edsr_x4_small", "edsr_x3_small", "edsr_x2_cfg1", "edsr_x4_canon", "duf_x4_canon", "drf_x4_canon",
-         "drf_sisr_x2_small"]
+         "drf_sisr_x2_small", "duf_x4_cond", "drf_x4_cond"]
+COND = {"duf_x4_cond", "drf_x4_cond"}
+
+
+def _proj(t, key, n):
+    """Same directions as oracle/make_golden.py proj() (seed = digest of the name)."""
+    seed = int.from_bytes(hashlib.sha256(key.encode()).digest()[:4], "little")
+    g = torch.Generator().manual_seed(seed)
+    flat = t.detach().double().flatten().cpu()
+    return torch.stack([torch.dot(flat, torch.randn(flat.numel(), generator=g, dtype=torch.float64))
+                        for _ in range(n)])
+
+
+def _rel(g, fx, k, full_key="grad_full64", proj_key="grad_proj64", norm_key="grad_norm64"):
+    """rel-L2 of g against the fixture's fp64 value: exact when stored in full,
+    else estimated from the projections."""
+    if k in fx[full_key]:
+        ref = fx[full_key][k].double()
+        return (g - ref).norm().item() / ref.norm().item()
+    e = _proj(g, k, fx["proj_n"]) - fx[proj_key][k]
+    return e.pow(2).mean().sqrt().item() / fx[norm_key][k]
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
@@ -109,14 +147,56 @@ def test_net_matches_golden(name, precision):
         if r32 is None:  # exact gradient is zero
             assert g.norm().item() <= (1e-4 if precision == "fp32" else 2e-2) * gmax, (k, g.norm().item())
             continue
-        if k in fx["grad_full64"]:
-            ref = fx["grad_full64"][k].double()
-            rel = (g - ref).norm().item() / ref.norm().item()
-        else:
-            n64 = fx["grad_norm64"][k]
-            rel = abs(g.norm().item() - n64) / n64
+        rel = _rel(g, fx, k)
         if precision == "fp32":
-            tol = max(1e-4, 3 * r32)
+            tol = 1e-4 if name in COND else max(1e-4, 3 * r32)
         else:
             tol = max(8e-2, 2 * fx["bf16_env"][k])
         assert rel <= tol, (k, rel, tol)
+
+
+def test_cond_fixtures_are_well_conditioned():
+    for name in COND:
+        fx = load_golden(name)
+        assert fx["act_margin"] >= 1e-5 and fx["cond_worst"] <= 2e-5, (name, fx["act_margin"], fx["cond_worst"])
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("name", ["duf_x4_canon", "duf_x4_cond", "edsr_x4_small", "drf_x4_cond"])
+def test_eval_forward_after_step(name, precision):
+    """Train step (updates BatchNorm running statistics), then net.eval() forward
+    against the fixture's eval output: exercises vsrk_bn_fold_running."""
+    fx = load_golden(name)
+    net = _build(fx, precision)
+    lr, hr = _to(fx["lr"]), _to(fx["hr"])
+    _l1(net(lr), hr).backward()
+    net.eval()
+    with torch.no_grad():
+        out = net(lr)
+    got, exp = _flat(out).cpu().double(), _flat(fx["output_eval"]).double()
+    d = (got - exp).abs()
+    if precision == "fp32":
+        assert d.max().item() <= 1e-4 * (1 + exp.abs().max().item()), d.max().item()
+    else:
+        assert d.max().item() <= 3e-2 * (1 + exp.abs().max().item()) and d.mean().item() <= 3e-3, (
+            d.max().item(), d.mean().item())
+
+
+@pytest.mark.parametrize("name", ["edsr_x4_small", "duf_x4_cond", "drf_x4_cond"])
+def test_adam_step_on_hip_gradients(name):
+    """One torch.optim.Adam step (main.py:73; fp32 master weights) on the fp32
+    HIP gradients reproduces the reference's update.  Adam's first step is
+    lr * g / (|g| + eps) per element, so only elements whose gradient is below
+    fp32 noise can differ (by up to 2 lr); rel-L2 of the update <= 1e-3."""
+    fx = load_golden(name)
+    net = _build(fx, "fp32")
+    lr, hr = _to(fx["lr"]), _to(fx["hr"])
+    _l1(net(lr), hr).backward()
+    a = fx["adam"]
+    opt = torch.optim.Adam(net.parameters(), lr=a["lr"], betas=tuple(a["betas"]), eps=a["eps"])
+    p0 = {k: p.detach().clone() for k, p in net.named_parameters()}
+    opt.step()
+    for k, p in net.named_parameters():
+        upd = (p.detach() - p0[k]).cpu().double()
+        rel = _rel(upd, fx, k, "adam_update_full", "adam_update_proj", "adam_update_norm")
+        assert rel <= 1e-3, (k, rel)

@@ -79,6 +79,7 @@ _SIGS = {
     "vsrk_duf_dynfilter_bwd": (C.c_int, [_P, _P, _P] + [C.c_int32] * 5 + [_P, _P, C.c_int32, _P]),
     "vsrk_conv_set_algo": (C.c_int, [C.c_int32]),
     "vsrk_conv_set_path": (C.c_int, [C.c_char_p, C.c_int32]),
+    "vsrk_conv_set_grid_cap": (C.c_int, [C.c_int32]),
     "vsrk_subpixel_conv_weight": (C.c_int, [_P, _P] + [C.c_int32] * 6 + [_P, _P, _P]),
     "vsrk_subpixel_wgrad_fold": (C.c_int, [_P, _P] + [C.c_int32] * 6 + [_P, _P, C.c_int32, _P]),
     "vsrk_prelu_workspace_size": (C.c_size_t, []),
@@ -112,6 +113,14 @@ def load(build_if_missing: bool = False):
                 raise RuntimeError(
                     f"vsrk native library not found at {path}; run `python -m vsr_amd.build` "
                     "(or __graft_entry__.build()) first — there is no CPU fallback")
+            _build.build()
+        elif path == _build.LIB and not _build.is_current():
+            # a library built from other sources would bind this module's
+            # struct layouts and signatures to different kernels
+            if not build_if_missing:
+                raise RuntimeError(
+                    f"vsrk native library {path} is stale (built from different sources than "
+                    f"vsr_amd/csrc); rebuild with `python -m vsr_amd.build`")
             _build.build()
         lib = C.CDLL(str(path))
         for name, (res, args) in _SIGS.items():

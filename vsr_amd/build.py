@@ -5,6 +5,7 @@ from __future__ import annotations
 
 import hashlib
 import os
+import re
 import subprocess
 from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
@@ -32,6 +33,29 @@ def _digest() -> str:
     return h.hexdigest()[:16]
 
 
+_INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _includes(src: Path) -> list[Path]:
+    """Local headers `src` includes, transitively, in a stable order."""
+    seen: dict[Path, None] = {}
+    todo = [src]
+    while todo:
+        cur = todo.pop()
+        for name in _INC.findall(cur.read_text()):
+            p = (cur.parent / name).resolve()
+            if p.exists() and p not in seen:
+                seen[p] = None
+                todo.append(p)
+    return sorted(seen)
+
+
+def is_current() -> bool:
+    """Whether libvsrk.so was built from the current sources and flags."""
+    stamp = LIBDIR / "libvsrk.stamp"
+    return LIB.exists() and stamp.exists() and stamp.read_text() == _digest()
+
+
 def build(force: bool = False, verbose: bool = False) -> Path:
     """Compile every ``csrc/*.hip`` and link ``libvsrk.so``; skipped when the
     sources are unchanged since the last build (digest stamp)."""
@@ -43,12 +67,12 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     objdir = LIBDIR / "obj"
     objdir.mkdir(exist_ok=True)
 
-    headers = b"".join(p.read_bytes() for p in sorted(CSRC.glob("*.h")) + [INCLUDE / "vsrk.h"])
-
     def compile_one(src: Path) -> Path:
         obj = objdir / (src.stem + ".o")
-        # per-object stamp: recompile only when this source, a header or the flags changed
-        key = hashlib.sha256(src.read_bytes() + headers + " ".join(FLAGS).encode()).hexdigest()[:16]
+        # per-object stamp: recompile only when this source, a header it
+        # includes (transitively) or the flags changed
+        deps = b"".join(p.read_bytes() for p in _includes(src))
+        key = hashlib.sha256(src.read_bytes() + deps + " ".join(FLAGS).encode()).hexdigest()[:16]
         ostamp = objdir / (src.stem + ".stamp")
         if not force and obj.exists() and ostamp.exists() and ostamp.read_text() == key:
             return obj

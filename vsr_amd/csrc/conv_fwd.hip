@@ -423,7 +423,7 @@ static int launch_fwd(ConvArgs a, hipStream_t s) {
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, NTHR, lds) != hipSuccess || per_cu < 1)
     per_cu = 1;
-  const int64_t grid = std::min<int64_t>(ntiles, (int64_t)num_cus() * per_cu);
+  const int64_t grid = vsrk_capped_grid(std::min<int64_t>(ntiles, (int64_t)num_cus() * per_cu));
   a.nblk = (int)grid;
   kern<<<a.nblk, NTHR, lds, s>>>(a);
   VSRK_LAUNCH_CHECK("conv_fwd");

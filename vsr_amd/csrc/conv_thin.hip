@@ -633,7 +633,7 @@ void launch_persistent(KF kern, ThinArgs& a, size_t lds, hipStream_t s) {
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, THR, lds) != hipSuccess || per_cu < 1)
     per_cu = 1;
-  const int want = num_cus_thin() * per_cu;
+  const int want = (int)vsrk_capped_grid(num_cus_thin() * per_cu);
   a.tiles_per_blk = ceil_div(a.ntiles, want);
   const int grid = ceil_div(a.ntiles, a.tiles_per_blk);
   kern<<<grid, THR, lds, s>>>(a);

@@ -366,6 +366,7 @@ static WgradPlan wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, cons
   }
   int want = target ? ceil_div(target, p.ncombos)
                     : std::min(ceil_div(512, p.ncombos), std::max(ceil_div(p.ntiles, 16), ceil_div(256, p.ncombos)));
+  if (vsrk_g_grid_cap > 0) want = std::max(1, vsrk_g_grid_cap / p.ncombos);
   want = std::max(1, std::min(want, p.ntiles));
   p.tps = ceil_div(p.ntiles, want);
   p.nsplit = ceil_div(p.ntiles, p.tps);

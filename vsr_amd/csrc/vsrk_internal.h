@@ -24,3 +24,9 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
 // path switches (vsrk_conv_set_path): -1 = from the environment, 0 off, 1 on
 extern int vsrk_g_thin_mode;
 extern int vsrk_g_wgrad_fast_mode;
+// vsrk_conv_set_grid_cap: > 0 caps the workgroups of the persistent conv grids
+// and of the weight-gradient split (tests drive the multi-tile loops with it)
+extern int vsrk_g_grid_cap;
+static inline int64_t vsrk_capped_grid(int64_t g) {
+  return vsrk_g_grid_cap > 0 ? std::max<int64_t>(1, std::min<int64_t>(g, vsrk_g_grid_cap)) : g;
+}

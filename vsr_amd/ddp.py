@@ -87,3 +87,35 @@ class GradSync:
         """Start from identical weights on every rank."""
         for p in self._params:
             dist.broadcast(p.data, src)
+        for b in self.net.buffers():
+            dist.broadcast(b.data, src)
+
+
+class SyncBNAllReduce:
+    """SyncBatchNorm hook for the fused BatchNorm3d of DUFNet (duf_net.py:116,
+    198,201,209,212 in the reference; train-mode batch statistics couple the
+    samples of a batch, so data-parallel ranks must share them).
+
+    ``hook(sums)`` sums the per-channel (sum, sumsq) -- or, in backward,
+    (sum_dy, sum_dy_xhat) -- over every rank in place (one small all-reduce
+    per BN layer, at most 2 x 256 floats) and returns the factor from the
+    local to the global voxel count.  Ranks hold equal-shaped shards (the
+    DistributedSampler pads the dataset to a multiple of the world size), so
+    that factor is the world size and no host sync is needed."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+
+    def __call__(self, t: torch.Tensor) -> int:
+        dist.all_reduce(t, group=self.group)
+        return self.world
+
+
+def enable_sync_bn(net, group=None) -> bool:
+    """Share BatchNorm batch statistics across the data-parallel ranks (a no-op
+    for nets without BatchNorm).  Returns whether the net has the hook."""
+    if not hasattr(net, "bn_allreduce"):
+        return False
+    net.bn_allreduce = SyncBNAllReduce(group) if dist.is_initialized() and dist.get_world_size(group) > 1 else None
+    return True

@@ -29,29 +29,37 @@ _ws: dict[int, torch.Tensor] = {}
 
 class KernelTimer:
     """Brackets selected native launches with HIP events on the launch stream
-    (torch's current stream, where every vsrk kernel runs).  `match(kind, x, y)`
-    selects launches; bench.py uses it for the roofline of the dominant kernel."""
+    (torch's current stream, where every vsrk kernel runs).  ``match(kind, xv,
+    yv)`` sees the launch kind (("conv_fwd" | "conv_wgrad", (kd, kh, kw))) and
+    its logical views (vsrk_tensor5: for a weight gradient the input and the
+    output gradient) and returns the launch's algorithmic FLOP, or 0 to skip
+    it.  bench.py uses it for the roofline of the dominant conv."""
 
     def __init__(self, match):
         self.match = match
-        self.events: list[tuple[torch.cuda.Event, torch.cuda.Event]] = []
+        self.events: list[tuple[torch.cuda.Event, torch.cuda.Event, float]] = []
         self.enabled = True
 
-    def wrap(self, kind, x, y, launch):
-        if not (self.enabled and self.match(kind, x, y)):
+    def wrap(self, kind, xv, yv, launch):
+        flop = self.match(kind, xv, yv) if self.enabled else 0
+        if not flop:
             return launch()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         out = launch()
         e.record()
-        self.events.append((s, e))
+        self.events.append((s, e, float(flop)))
         return out
 
-    def mean_ms(self) -> float:
+    def totals(self) -> tuple[float, float, int]:
+        """(total FLOP, total seconds, launches) of the matched launches."""
         torch.cuda.synchronize()
-        if not self.events:
-            return float("nan")
-        return sum(s.elapsed_time(e) for s, e in self.events) / len(self.events)
+        t = sum(s.elapsed_time(e) for s, e, _ in self.events) * 1e-3
+        return sum(f for _, _, f in self.events), t, len(self.events)
+
+    def mean_ms(self) -> float:
+        flop, t, n = self.totals()
+        return t / n * 1e3 if n else float("nan")
 
 
 timer: KernelTimer | None = None
@@ -128,7 +136,7 @@ def conv(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, *, bias: to
                                  N.ptr(pro_shift), C.byref(rv) if rv is not None else None,
                                  C.byref(mv) if mv is not None else None, C.byref(yv), N.stream_ptr(x.device))
 
-    rc = timer.wrap(("conv_fwd", tuple(k)), x, y, launch) if timer is not None else launch()
+    rc = timer.wrap(("conv_fwd", tuple(k)), xv, yv, launch) if timer is not None else launch()
     N.check(rc, "conv_fwd")
     return y
 
@@ -150,13 +158,19 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, k, pad, dw: torch.Tensor, dbia
                                    float(dy_scale), perm_r, dw.data_ptr(), N.ptr(dbias), 1 if accumulate else 0,
                                    ws.data_ptr(), ws.numel(), N.stream_ptr(x.device))
 
-    rc = timer.wrap(("conv_wgrad", tuple(k)), x, dy, launch) if timer is not None else launch()
+    rc = timer.wrap(("conv_wgrad", tuple(k)), xv, gv, launch) if timer is not None else launch()
     N.check(rc, "conv_wgrad")
 
 
 def set_conv_path(path: str, mode: int) -> None:
     """Select a conv kernel family ("fast", "thin", "wgrad_fast"): -1 default, 0 off, 1 on."""
     N.check(_lib().vsrk_conv_set_path(path.encode(), int(mode)), "conv_set_path")
+
+
+def set_grid_cap(max_workgroups: int) -> None:
+    """Cap the persistent conv grids / wgrad split (0 = default); tests use it to
+    run many tiles per workgroup at small shapes."""
+    N.check(_lib().vsrk_conv_set_grid_cap(int(max_workgroups)), "conv_set_grid_cap")
 
 
 def to_view(src: torch.Tensor, dtype: torch.dtype, cpad: int | None = None) -> torch.Tensor:

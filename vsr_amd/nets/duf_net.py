@@ -111,13 +111,18 @@ class DUFNet(BaseNet):
 
     def _bn_backward(self, bn, x, dz, st, dx, accumulate, grads):
         red = F.bn_relu_bwd_reduce(x, dz, st)
-        if self.bn_allreduce is not None:
-            self.bn_allreduce(red)
-        F.bn_relu_bwd_apply(x, dz, st, bn.weight, red, st.count, dx, accumulate)
+        # dgamma / dbeta are this rank's local sums: the data-parallel gradient
+        # average (GradSync) combines them across ranks, as torch's
+        # SyncBatchNorm does.  Only the copy that feeds the input gradient is
+        # all-reduced (sum over the global batch, with the global count).
         gw = self._grad_buffer(bn.weight)
         gb = self._grad_buffer(bn.bias)
         gw.copy_(red[1])
         gb.copy_(red[0])
+        if self.bn_allreduce is not None:
+            red = red.clone()
+            self.bn_allreduce(red)
+        F.bn_relu_bwd_apply(x, dz, st, bn.weight, red, st.count, dx, accumulate)
         self._grad_done(grads, bn.weight, gw)
         self._grad_done(grads, bn.bias, gb)
 

@@ -17,8 +17,17 @@ SISR, SISR-SRFB, MISR and VSR subclasses.  What changes, and why:
   * Metrics run fused: PSNR / SSIM of denormalized images (utils.py:1-20 then
     metrics.py) are single HIP kernels with the denormalize inside.
   * Data parallel: an optional ``grad_sync`` (vsr_amd.ddp.GradSync) is
-    finished between backward and optimizer.step(); logs are all-reduced
-    (sum) across ranks once per epoch.
+    finished between backward and optimizer.step(); BatchNorm statistics are
+    synchronised across ranks (vsr_amd.ddp.enable_sync_bn) whenever a process
+    group with more than one rank is up; the loaders' DistributedSampler
+    (vsr_amd.data.Dataloader) gets set_epoch each epoch; logs are
+    all-reduced (sum) across ranks once per epoch; checkpoints are written by
+    rank 0 only.
+  * Checkpoints keep the reference's schema but store the monitor as plain
+    state, so ``load`` uses torch.load(weights_only=True) -- also for
+    checkpoints written by the reference, whose pickled Monitor is mapped
+    onto vsr_amd.callbacks.Monitor by an allow-list (nothing in the file is
+    executed).
   * ReduceLROnPlateau: base_trainer.py:67 tests an undefined ``mode`` (a
     NameError whenever that scheduler is used); it is stepped here with the
     validation loss, which is what the branch evidently intends.
@@ -37,6 +46,8 @@ import torch
 import torch.distributed as dist
 
 from .. import metrics as M
+from ..callbacks.monitor import Monitor, safe_globals
+from ..ddp import enable_sync_bn
 from ..utils import denormalize
 
 
@@ -75,6 +86,8 @@ class BaseTrainer:
         self.epoch = 1
         self.np_random_seeds = None
         self.grad_sync = grad_sync
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            enable_sync_bn(self.net)
         self._denormalize = functools.partial(denormalize, dataset=self.dataset)
 
     # ------------------------------------------------------------------
@@ -83,6 +96,9 @@ class BaseTrainer:
             self.np_random_seeds = random.sample(range(10000000), k=self.num_epochs)
         while self.epoch <= self.num_epochs:
             np.random.seed(self.np_random_seeds[self.epoch - 1])
+            for dl in (self.train_dataloader, self.valid_dataloader):
+                if hasattr(dl, "set_epoch"):
+                    dl.set_epoch(self.epoch)
             logging.info(f'Epoch {self.epoch}.')
             train_log, train_batch, train_outputs = self._run_epoch('training')
             logging.info(f'Train log: {train_log}.')
@@ -202,26 +218,41 @@ class BaseTrainer:
 
     def save(self, path):
         """Same checkpoint schema as base_trainer.py:224-237 (state_dict keys of the
-        unwrapped net, so reference and vsr_amd checkpoints interoperate)."""
+        unwrapped net, so reference and vsr_amd checkpoints interoperate); the
+        monitor is stored as its state_dict (plain types).  Rank 0 writes."""
+        if dist.is_available() and dist.is_initialized() and dist.get_rank() != 0:
+            return
+        mon = self.monitor
         torch.save({
             'net': self.net.state_dict(),
             'optimizer': self.optimizer.state_dict(),
             'lr_scheduler': self.lr_scheduler.state_dict() if self.lr_scheduler else None,
-            'monitor': self.monitor,
+            'monitor': mon.state_dict() if hasattr(mon, "state_dict") else mon,
             'epoch': self.epoch,
             'random_state': random.getstate(),
             'np_random_seeds': self.np_random_seeds,
         }, path)
 
     def load(self, path):
-        """base_trainer.py:239-252.  The checkpoint holds the pickled monitor, so
-        only load checkpoints written by a trainer you ran."""
-        checkpoint = torch.load(path, map_location=self.device, weights_only=False)
+        """base_trainer.py:239-252, with torch.load(weights_only=True)."""
+        with torch.serialization.safe_globals(safe_globals()):
+            checkpoint = torch.load(path, map_location=self.device, weights_only=True)
         self.net.load_state_dict(checkpoint['net'])
         self.optimizer.load_state_dict(checkpoint['optimizer'])
         if checkpoint['lr_scheduler']:
             self.lr_scheduler.load_state_dict(checkpoint['lr_scheduler'])
-        self.monitor = checkpoint['monitor']
+        state = checkpoint['monitor']
+        if state is not None:
+            if self.monitor is None:
+                d = state if isinstance(state, dict) else vars(state)
+                self.monitor = Monitor(d['checkpoints_dir'], d['mode'], d['target'], d['saved_freq'])
+            if hasattr(self.monitor, "load_state_dict"):
+                self.monitor.load_state_dict(state)
+            else:  # a caller-supplied monitor object: restore its attributes
+                d = state if isinstance(state, dict) else vars(state)
+                for k, v in d.items():
+                    if k != "checkpoints_dir":
+                        setattr(self.monitor, k, v)
         self.epoch = checkpoint['epoch'] + 1
         random.setstate(checkpoint['random_state'])
         self.np_random_seeds = checkpoint['np_random_seeds']
