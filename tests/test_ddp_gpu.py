@@ -81,10 +81,11 @@ def _worker(rank, world, port, model, q):
         out = net(xs)
         _loss(out, ys).backward()
         sync.finish()
-        outs = [o.detach().cpu() for o in out] if isinstance(out, list) else out.detach().cpu()
-        res = {"grads": {k: p.grad.detach().cpu().clone() for k, p in net.named_parameters()},
+        # numpy arrays travel by value (a shared-memory tensor would outlive its sender)
+        outs = [o.detach().cpu().numpy() for o in out] if isinstance(out, list) else out.detach().cpu().numpy()
+        res = {"grads": {k: p.grad.detach().cpu().numpy() for k, p in net.named_parameters()},
                "out": outs,
-               "buffers": {k: v.detach().cpu().clone() for k, v in net.state_dict().items() if "running" in k}}
+               "buffers": {k: v.detach().cpu().numpy() for k, v in net.state_dict().items() if "running" in k}}
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -111,6 +112,10 @@ def test_two_ranks_equal_one_process(model):
     for p in procs:
         p.start()
     got = dict(q.get(timeout=180) for _ in range(2))
+    for r in got.values():
+        r["grads"] = {k: torch.from_numpy(v) for k, v in r["grads"].items()}
+        r["buffers"] = {k: torch.from_numpy(v) for k, v in r["buffers"].items()}
+        r["out"] = [torch.from_numpy(v) for v in r["out"]] if isinstance(r["out"], list) else torch.from_numpy(r["out"])
     for p in procs:
         p.join(60)
         assert p.exitcode == 0

@@ -14,6 +14,9 @@ CASES = {
     # name: (N, D, H, W, Cin, Cout, k, pad)
     "edsr3x3": (64, 1, 128, 128, 64, 64, (1, 3, 3), (0, 1, 1)),
     "duf3x3x3": (4, 16, 128, 128, 64, 32, (3, 3, 3), (1, 1, 1)),
+    # the bench's DUF unit convs: 64 windows x 7 frames
+    "duf64": (64, 7, 128, 128, 64, 32, (3, 3, 3), (1, 1, 1)),
+    "duf224v": (64, 7, 128, 128, 224, 32, (3, 3, 3), (0, 1, 1)),
     "duf1x1x1": (64, 7, 128, 128, 128, 128, (1, 1, 1), (0, 0, 0)),
     # EDSR tail conv F -> 1 at HR (thin-channel kernels: fwd = thin-out, dgrad = thin-in)
     "tail": (64, 1, 512, 512, 64, 1, (1, 3, 3), (0, 1, 1)),
@@ -35,8 +38,12 @@ def main():
     ap.add_argument("--case", default="edsr3x3")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--what", default="fwd,res,wgrad")
+    ap.add_argument("--paths", default="", help="e.g. k3=0,fast=1 (vsrk_conv_set_path)")
     args = ap.parse_args()
     _native.load()
+    for kv in filter(None, args.paths.split(",")):
+        p, m = kv.split("=")
+        F.set_conv_path(p, int(m))
     dev = "cuda"
     n, d, h, w, ci, co, k, pad = CASES[args.case]
     dt = torch.bfloat16

@@ -43,7 +43,8 @@ extern "C" int vsrk_conv_set_path(const char* path, int32_t mode) {
   if (p == "fast") g_fast_mode = mode;
   else if (p == "thin") vsrk_g_thin_mode = mode;
   else if (p == "wgrad_fast") vsrk_g_wgrad_fast_mode = mode;
-  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, thin, wgrad_fast)", path);
+  else if (p == "k3") vsrk_g_k3_mode = mode;
+  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, k3, thin, wgrad_fast)", path);
   return VSRK_OK;
 }
 
@@ -64,6 +65,7 @@ int vsrk_conv_fwd_fast(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   }
   if (g_fast_mode == 0) return 0;
   if (x->dtype != VSRK_BF16) return 0;
+  if (const int k3 = vsrk_conv_fwd_k3(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s)) return k3;
   if (!chunk_ok(x, 2) || x->c % 8 != 0) return 0;
   const int xr = x->shuffle > 1 ? x->shuffle : 1, yr = y->shuffle > 1 ? y->shuffle : 1;
   if (xr > 1 && (x->c / (xr * xr)) % 32 != 0) return 0;

@@ -21,7 +21,13 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                        const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
 
+// second-generation 3x3(x3) bf16 conv (conv_k3.hip); same return convention
+int vsrk_conv_fwd_k3(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                     const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
+                     const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
+
 // path switches (vsrk_conv_set_path): -1 = from the environment, 0 off, 1 on
+extern int vsrk_g_k3_mode;
 extern int vsrk_g_thin_mode;
 extern int vsrk_g_wgrad_fast_mode;
 // vsrk_conv_set_grid_cap: > 0 caps the workgroups of the persistent conv grids
