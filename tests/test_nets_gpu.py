@@ -202,5 +202,13 @@ def test_adam_step_on_hip_gradients(name):
         if fx["ref32_err"][k] is None:  # exact gradient 0 (a conv bias feeding a BatchNorm): the
             continue                    # update is lr * noise / (|noise| + eps), no reference value
         upd = (p.detach() - p0[k]).cpu().double()
-        rel = _rel(upd, fx, k, "adam_update_full", "adam_update_proj", "adam_update_norm")
+        if k in fx["adam_update_full"] and k in fx["grad_full64"]:
+            # elements whose exact gradient is 0 (e.g. a bias fed by an L1 loss whose signs
+            # cancel) get lr * noise / (|noise| + eps): no reference value, left out
+            gref, uref = fx["grad_full64"][k].double(), fx["adam_update_full"][k].double()
+            keep = gref.abs() > 1e-6 * gref.abs().max()
+            assert (upd.abs() <= a["lr"] * 1.001).all(), k
+            rel = ((upd - uref)[keep].norm() / uref[keep].norm()).item()
+        else:
+            rel = _rel(upd, fx, k, "adam_update_full", "adam_update_proj", "adam_update_norm")
         assert rel <= 1e-3, (k, rel)
