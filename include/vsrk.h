@@ -228,8 +228,15 @@ int vsrk_ssim(const float* out, const float* target, int32_t batch, int32_t chan
  *                     shift = beta - mean*scale (the fused conv prologue's
  *                     VSRK_PRO_AFFINE_RELU operands), running stats updated
  *                     with momentum and the unbiased variance (torch semantics)
- *   vsrk_bn_fold_running: eval mode (running statistics)
- * Backward of BN followed by ReLU, given dz = dL/d relu(bn(x)):
+ *   vsrk_bn_fold_running: eval mode (running statistics); mean / invstd
+ *                     (may be NULL) receive running_mean, 1/sqrt(running_var + eps)
+ *                     for the eval-mode backward (call the backward pair with
+ *                     count = INFINITY: no batch-statistics terms)
+ *   vsrk_bn_apply:    y = x * scale + shift [relu] (a materialised BatchNorm3d
+ *                     output, for op-level use; the generators fold it into
+ *                     the next conv instead)
+ * Backward of BN followed by ReLU, given dz = dL/d relu(bn(x)) (a BN without
+ * ReLU: pass scale = 0, shift = 1 -- the ReLU mask is x * scale + shift > 0):
  *   vsrk_bn_relu_bwd_reduce: sum_dy, sum_dy_xhat (= dbeta, dgamma)
  *   vsrk_bn_relu_bwd_apply:  dx [+]= gamma*invstd*(dy - sum_dy/M - xhat*sum_dy_xhat/M)
  * Workspace: vsrk_bn_workspace_size(channels) bytes. */
@@ -240,8 +247,10 @@ int vsrk_bn_finalize(const float* sum, const float* sumsq, double count, const f
                      float eps, float momentum, float* running_mean, float* running_var, float* scale,
                      float* shift, float* mean, float* invstd, int32_t channels, void* stream);
 int vsrk_bn_fold_running(const float* gamma, const float* beta, const float* running_mean,
-                         const float* running_var, float eps, float* scale, float* shift, int32_t channels,
-                         void* stream);
+                         const float* running_var, float eps, float* scale, float* shift, float* mean,
+                         float* invstd, int32_t channels, void* stream);
+int vsrk_bn_apply(const vsrk_tensor5* x, const float* scale, const float* shift, int32_t relu, const vsrk_tensor5* y,
+                  void* stream);
 int vsrk_bn_relu_bwd_reduce(const vsrk_tensor5* x, const vsrk_tensor5* dz, const float* scale, const float* shift,
                             const float* mean, const float* invstd, float* sum_dy, float* sum_dy_xhat,
                             void* workspace, size_t workspace_bytes, void* stream);

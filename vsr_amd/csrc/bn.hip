@@ -177,13 +177,16 @@ __global__ void bn_finalize_kernel(const float* __restrict__ sum, const float* _
 // eval mode: fold running statistics
 __global__ void bn_fold_running_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
                                        const float* __restrict__ rmean, const float* __restrict__ rvar, float eps,
-                                       float* __restrict__ scale, float* __restrict__ shift, int C) {
+                                       float* __restrict__ scale, float* __restrict__ shift,
+                                       float* __restrict__ mean, float* __restrict__ invstd, int C) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const float is = 1.f / sqrtf(rvar[c] + eps);
   const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
   scale[c] = g * is;
   shift[c] = b - rmean[c] * g * is;
+  if (mean) mean[c] = rmean[c];
+  if (invstd) invstd[c] = is;
 }
 
 // dx [+]= gamma*invstd*(dy - sum_dy/M - xhat*sum_dy_xhat/M), dy = dz*(x*scale+shift > 0),
@@ -258,6 +261,55 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(View x, View dz,
   }
 }
 
+// y = x * scale + shift [relu] per channel (the standalone BatchNorm3d forward
+// of the op-level modules; the generators fold it into the next conv instead)
+template <typename T>
+__global__ __launch_bounds__(256) void bn_apply_kernel(View x, View y, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, int relu, int nrows) {
+  constexpr int E = Chunk<T>::E;
+  const int C = x.c;
+  const int cpv = (C + E - 1) / E;
+  const int vpb = blockDim.x / cpv;
+  const int ch = threadIdx.x % cpv, vl = threadIdx.x / cpv;
+  if (vl >= vpb) return;
+  const int c0 = ch * E;
+  const bool full = c0 + E <= C;
+  float sc[E], sh[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int c = min(c0 + e, C - 1);
+    sc[e] = scale[c];
+    sh[e] = shift[c];
+  }
+  for (int r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const T* xr = reinterpret_cast<const T*>(x.ptr) + row_off(x, r) + c0;
+    T* yr = reinterpret_cast<T*>(y.ptr) + row_off(y, r) + c0;
+    for (int w = vl; w < x.w; w += vpb) {
+      const T* px = xr + (int64_t)w * x.sw;
+      T* py = yr + (int64_t)w * y.sw;
+      float f[E];
+      if (full) {
+        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(px), f);
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) f[e] = c0 + e < C ? to_f32<T>(px[e]) : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const float t = fmaf(f[e], sc[e], sh[e]);
+        f[e] = relu ? fmaxf(t, 0.f) : t;
+      }
+      if (full) {
+        *reinterpret_cast<uint4*>(py) = Chunk<T>::pack(f);
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (c0 + e < C) py[e] = from_f32<T>(f[e]);
+      }
+    }
+  }
+}
+
 int reduce_launch(int mode, const vsrk_tensor5* x, const vsrk_tensor5* dz, const float* scale, const float* shift,
                   const float* mean, const float* invstd, float* o1, float* o2, void* ws, size_t ws_bytes,
                   hipStream_t s) {
@@ -315,11 +367,11 @@ extern "C" int vsrk_bn_finalize(const float* sum, const float* sumsq, double cou
 }
 
 extern "C" int vsrk_bn_fold_running(const float* gamma, const float* beta, const float* running_mean,
-                                    const float* running_var, float eps, float* scale, float* shift,
-                                    int32_t channels, void* stream) {
+                                    const float* running_var, float eps, float* scale, float* shift, float* mean,
+                                    float* invstd, int32_t channels, void* stream) {
   VSRK_CHECK(running_mean && running_var && scale && shift, "bn_fold_running: null argument");
   bn_fold_running_kernel<<<ceil_div(channels, 256), 256, 0, (hipStream_t)stream>>>(
-      gamma, beta, running_mean, running_var, eps, scale, shift, channels);
+      gamma, beta, running_mean, running_var, eps, scale, shift, mean, invstd, channels);
   VSRK_LAUNCH_CHECK("bn_fold_running");
   return VSRK_OK;
 }
@@ -362,5 +414,29 @@ extern "C" int vsrk_bn_relu_bwd_apply(const vsrk_tensor5* x, const vsrk_tensor5*
                                                          mean, invstd, gamma, sum_dy, sum_dy_xhat,
                                                          (float)(1.0 / count), nrows, accumulate);
   VSRK_LAUNCH_CHECK("bn_relu_bwd_apply");
+  return VSRK_OK;
+}
+
+extern "C" int vsrk_bn_apply(const vsrk_tensor5* x, const float* scale, const float* shift, int32_t relu,
+                             const vsrk_tensor5* y, void* stream) {
+  VSRK_CHECK(x && y && x->ptr && y->ptr && scale && shift, "bn_apply: null argument");
+  VSRK_CHECK(x->dtype == y->dtype && x->c == y->c && x->n == y->n && x->d == y->d && x->h == y->h && x->w == y->w &&
+                 x->shuffle <= 1 && y->shuffle <= 1,
+             "bn_apply: view mismatch");
+  const int E = x->dtype == VSRK_BF16 ? 8 : 4;
+  const int cpv = ceil_div(x->c, E);
+  VSRK_CHECK(cpv <= 256, "bn_apply: too many channels (%d)", x->c);
+  const int64_t nr64 = (int64_t)x->n * x->d * x->h;
+  VSRK_CHECK(nr64 < (1ll << 31), "bn_apply: too many rows");
+  const int nrows = (int)nr64;
+  if (nrows == 0) return VSRK_OK;
+  const int thr = cpv * (256 / cpv);
+  const int grid = std::min(nrows, 4096);
+  hipStream_t s = (hipStream_t)stream;
+  if (x->dtype == VSRK_BF16)
+    bn_apply_kernel<bf16><<<grid, thr, 0, s>>>(make_view(x), make_view(y), scale, shift, relu, nrows);
+  else
+    bn_apply_kernel<float><<<grid, thr, 0, s>>>(make_view(x), make_view(y), scale, shift, relu, nrows);
+  VSRK_LAUNCH_CHECK("bn_apply");
   return VSRK_OK;
 }

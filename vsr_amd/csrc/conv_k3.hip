@@ -42,7 +42,7 @@ int vsrk_conv_fwd_k3(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
   if (y->c % 8 != 0 || (yr > 1 && (y->c / (yr * yr)) % 8 != 0)) return 0;
   if (!aligned16(x) || !aligned16(y)) return 0;
   if (xr > 1 && (d->prologue || yr > 1)) return 0;
-  if (yr > 1 && (residual || mask)) return 0;
+  if (yr > 1 && (residual || mask || (y->c / (yr * yr)) % 64 != 0)) return 0;
   for (const vsrk_tensor5* t : {residual, mask}) {
     if (t && (!aligned16(t) || t->shuffle > 1 || t->dtype != VSRK_BF16)) return 0;
   }

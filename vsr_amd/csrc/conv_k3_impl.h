@@ -121,6 +121,80 @@ __device__ __forceinline__ void bdma16(i32x4 rsrc, uint32_t voff, uint32_t soff,
         "s"(__builtin_amdgcn_readfirstlane(lds_base)));
 }
 
+// N LDS-DMA pieces in one statement (one M0 save / restore): piece k loads
+// rsrc[v[k] + soff] into LDS at m0_base + k * STEP.
+template <int N, int STEP>
+__device__ __forceinline__ void bdma16xN(i32x4 rsrc, const uint32_t* v, uint32_t soff, uint32_t m0_base) {
+  static_assert(N >= 1 && N <= 5, "1..5 pieces");
+  unsigned keep;
+  const uint32_t so = __builtin_amdgcn_readfirstlane(soff), mb = __builtin_amdgcn_readfirstlane(m0_base);
+  if constexpr (N == 1) {
+    asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %4\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(v[0]), "s"(rsrc), "s"(so), "s"(mb), "n"(STEP));
+  }
+  if constexpr (N == 2) {
+    asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %5\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, %4 offen lds\n\t"
+      "s_add_u32 m0, m0, %6\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(v[0]), "v"(v[1]), "s"(rsrc), "s"(so), "s"(mb), "n"(STEP));
+  }
+  if constexpr (N == 3) {
+    asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %6\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %4, %5 offen lds\n\t"
+      "s_add_u32 m0, m0, %7\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %4, %5 offen lds\n\t"
+      "s_add_u32 m0, m0, %7\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %3, %4, %5 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(v[0]), "v"(v[1]), "v"(v[2]), "s"(rsrc), "s"(so), "s"(mb), "n"(STEP));
+  }
+  if constexpr (N == 4) {
+    asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %7\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %5, %6 offen lds\n\t"
+      "s_add_u32 m0, m0, %8\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %5, %6 offen lds\n\t"
+      "s_add_u32 m0, m0, %8\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %3, %5, %6 offen lds\n\t"
+      "s_add_u32 m0, m0, %8\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %4, %5, %6 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "s"(rsrc), "s"(so), "s"(mb), "n"(STEP));
+  }
+  if constexpr (N == 5) {
+    asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %8\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %6, %7 offen lds\n\t"
+      "s_add_u32 m0, m0, %9\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %6, %7 offen lds\n\t"
+      "s_add_u32 m0, m0, %9\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %3, %6, %7 offen lds\n\t"
+      "s_add_u32 m0, m0, %9\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %4, %6, %7 offen lds\n\t"
+      "s_add_u32 m0, m0, %9\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %5, %6, %7 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "s"(rsrc), "s"(so), "s"(mb), "n"(STEP));
+  }
+}
+
 // 8 consecutive channels per lane after the permlane32 swap
 __device__ __forceinline__ void unpack8(uint4 v, float* f) { Chunk<bf16>::unpack(v, f); }
 
@@ -151,7 +225,8 @@ __global__ __launch_bounds__(K3_NW * 64, 2) void conv_k3_kernel(K3Args a) {
   if constexpr (PRO) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, a.cin_pad, tid, K3_NW * 64);
 
   // B DMA roles, fixed: instruction j = wave + 4k holds entries j*64 + lane
-  // -> (plane, tap, co) of the packed weight [tap][cout_pad][cin_pad]
+  // -> (plane, tap, co) of the packed weight [tap][cout_pad][cin_pad]; waves
+  // below BI % 4 issue NBW pieces, the others NBW - 1
   uint32_t b_off[NBW];
 #pragma unroll
   for (int k = 0; k < NBW; ++k) {
@@ -160,6 +235,7 @@ __global__ __launch_bounds__(K3_NW * 64, 2) void conv_k3_kernel(K3Args a) {
     const int tap = rem / NT, co = rem - (rem / NT) * NT;
     b_off[k] = pl < 2 ? (uint32_t)(2 * ((tap * a.cout_pad + co) * a.cin_pad + 8 * pl)) : K3_OOB;
   }
+  const bool b_full = (BI % K3_NW) == 0 || wave < (BI % K3_NW);
   const i32x4 wrsrc = make_rsrc(a.w);
   const uint32_t lds0 = lds_addr(lds);
   const uint32_t a_rd = (uint32_t)(((hf * K3_NVP) + wave * K3_R * K3_HC + l32) * 16);
@@ -221,17 +297,11 @@ __global__ __launch_bounds__(K3_NW * 64, 2) void conv_k3_kernel(K3Args a) {
     }
     const uint32_t soa = (uint32_t)(2 * xo);
     const uint32_t sob = (uint32_t)(2 * (((int64_t)kdi * 9 * a.cout_pad + n0) * a.cin_pad + c0));
-    const uint32_t base = lds0 + slot * SLOT;
-#pragma unroll
-    for (int k = 0; k < NAW; ++k) {
-      const int i = wave + K3_NW * k;
-      if (i < K3_AI) bdma16(xrsrc, voff[k], soa, base + i * 1024);
-    }
-#pragma unroll
-    for (int k = 0; k < NBW; ++k) {
-      const int j = wave + K3_NW * k;
-      if (j < BI) bdma16(wrsrc, b_off[k], sob, base + K3_ABYTES + j * 1024);
-    }
+    const uint32_t base = lds0 + slot * SLOT + wave * 1024;
+    static_assert(NAW == 5 && K3_AI == 20, "A staging: five pieces per wave");
+    bdma16xN<5, K3_NW * 1024>(xrsrc, voff, soa, base);
+    if (b_full) bdma16xN<NBW, K3_NW * 1024>(wrsrc, b_off, sob, base + K3_ABYTES);
+    else bdma16xN<NBW - 1, K3_NW * 1024>(wrsrc, b_off, sob, base + K3_ABYTES);
     return c0;
   };
 
@@ -293,6 +363,9 @@ __global__ __launch_bounds__(K3_NW * 64, 2) void conv_k3_kernel(K3Args a) {
       c0n = issue(last ? 0 : s + 1, slot ^ 1);
     }
     // MFMAs of stage s: per kw, 6 halo-row A fragments and 3 x NS B fragments
+    // (raised issue priority: the other workgroup's wave on this SIMD takes
+    // the gaps for its DMA / epilogue instructions)
+    __builtin_amdgcn_s_setprio(1);
     {
       const char* sA = lds + slot * SLOT;
 #pragma unroll
@@ -314,26 +387,46 @@ __global__ __launch_bounds__(K3_NW * 64, 2) void conv_k3_kernel(K3Args a) {
             for (int ns = 0; ns < NS; ++ns) mma<bf16>(acc[r][ns], bw[kh][ns], af[r + kh]);
       }
     }
+    __builtin_amdgcn_s_setprio(0);
     if (last) {
-      // Epilogue: after swapping register groups between the lane halves,
-      // lane (l32, hf) holds for accumulator (r, ns) and group pair q the 8
-      // output channels n0 + ns*32 + q*16 + hf*8 .. +8 of voxel
-      // (h0 + wave*4 + r, w0 + l32): every access is 16 contiguous bytes.
+      // Epilogue.  Per register: bias (pre-scaled), out_scale, activation
+      // (register 4g + e is channel 8g + 4hf + e); then v_permlane32_swap
+      // vdst, src -- it exchanges lanes 32-63 of vdst with lanes 0-31 of src --
+      // with vdst = group 2q, src = group 2q+1: the low half ends up with
+      // channels 16q .. 16q+7 (own 2q | upper's 2q), the high half with
+      // 16q+8 .. 16q+15 (lower's 2q+1 | own 2q+1), so each lane finishes 8
+      // consecutive channels of its voxel with 16-byte accesses at a per-row
+      // base + immediate offsets.  (Inline asm: hipcc's builtin lowering fed
+      // both operands from one register here.)
       const int wo = e_w0 + l32;
+      const bool ok_w = wo < a.y.w;
+      int64_t ybase, rbase = 0, mbase = 0;
+      if constexpr (YS) {  // sub-pixel store: the tile's 64 channels are one sub-pixel (cphys % 64 == 0)
+        const int sub = e_n0 / a.y.cphys, cc0 = e_n0 - sub * a.y.cphys;
+        const int si = sub / yr, sj = sub - si * yr;
+        ybase = e_nb * a.y.sn + (int64_t)e_dz * a.y.sd + (int64_t)si * a.y.sh + (int64_t)(wo * yr + sj) * a.y.sw + cc0;
+      } else {
+        ybase = e_nb * a.y.sn + (int64_t)e_dz * a.y.sd + (int64_t)wo * a.y.sw + e_n0;
+        rbase = e_nb * a.res.sn + (int64_t)e_dz * a.res.sd + (int64_t)wo * a.res.sw + e_n0;
+        mbase = e_nb * a.msk.sn + (int64_t)e_dz * a.msk.sd + (int64_t)wo * a.msk.sw + e_n0;
+      }
+      const int64_t ysh = (int64_t)yr * a.y.sh;
 #pragma unroll
       for (int r = 0; r < K3_R; ++r) {
         const int ho = e_h0 + wave * K3_R + r;
+        if (ho >= a.y.h) {  // wave-uniform
+#pragma unroll
+          for (int ns = 0; ns < NS; ++ns)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[r][ns][i] = 0.f;
+          continue;
+        }
+        bf16* yrow = reinterpret_cast<bf16*>(a.y.ptr) + ybase + ho * ysh + hf * 8;
+        const bf16* rrow = reinterpret_cast<const bf16*>(a.res.ptr) + rbase + (int64_t)ho * a.res.sh + hf * 8;
+        const bf16* mrow = reinterpret_cast<const bf16*>(a.msk.ptr) + mbase + (int64_t)ho * a.msk.sh + hf * 8;
 #pragma unroll
         for (int ns = 0; ns < NS; ++ns) {
           f32x16& A = acc[r][ns];
-          // bias, out_scale and activation per register (channel 8g + 4hf + e of
-          // register 4g + e), then v_permlane32_swap vdst, src -- it exchanges
-          // lanes 32-63 of vdst with lanes 0-31 of src -- with vdst = group 2q,
-          // src = group 2q+1: the low half ends up with channels 16q .. 16q+7
-          // (own 2q | upper's 2q), the high half with 16q+8 .. 16q+15 (lower's
-          // 2q+1 | own 2q+1).  Inline asm: hipcc's builtin lowering fed both
-          // operands from one register here; s_nop 1 covers the VALU-write ->
-          // permlane-read hazard.
           float v[16];
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
@@ -341,63 +434,43 @@ __global__ __launch_bounds__(K3_NW * 64, 2) void conv_k3_kernel(K3Args a) {
             const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              float tq = fmaf(A[4 * g + e], a.out_scale, bb[e]);
+              const float tq = fmaf(A[4 * g + e], a.out_scale, bb[e]);
               v[4 * g + e] = act ? act_apply(a.act, tq, aslope) : tq;
             }
-          }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(v[e]), "+v"(v[4 + e]));
-            asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(v[8 + e]), "+v"(v[12 + e]));
-          }
-          if (ho < a.y.h) {  // wave-uniform
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-              const int co = e_n0 + ns * 32 + q * 16 + hf * 8;
-              const bool ok = wo < a.y.w && co < a.cout;
-              int64_t yoff;
-              if constexpr (YS) {
-                const int sub = co / a.y.cphys, cc = co - sub * a.y.cphys;
-                const int si = sub / yr, sj = sub - si * yr;
-                yoff = e_nb * a.y.sn + (int64_t)e_dz * a.y.sd + (int64_t)(ho * yr + si) * a.y.sh +
-                       (int64_t)(wo * yr + sj) * a.y.sw + cc;
-              } else {
-                yoff = e_nb * a.y.sn + (int64_t)e_dz * a.y.sd + (int64_t)ho * a.y.sh + (int64_t)wo * a.y.sw + co;
-              }
-              bf16* yp = reinterpret_cast<bf16*>(a.y.ptr) + yoff;
-              float tv[8];
-#pragma unroll
-              for (int e = 0; e < 8; ++e) tv[e] = v[q * 8 + e];
-              if (use_msk) {
-                float m[8];
-                uint4 mv = make_uint4(0, 0, 0, 0);
-                if (ok)
-                  mv = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.msk.ptr) +
-                                                       (e_nb * a.msk.sn + (int64_t)e_dz * a.msk.sd +
-                                                        (int64_t)ho * a.msk.sh + (int64_t)wo * a.msk.sw + co));
-                unpack8(mv, m);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) tv[e] = mask_apply(m[e], tv[e], mslope);
-              }
-              if (use_res) {
-                float rr[8];
-                uint4 rv = make_uint4(0, 0, 0, 0);
-                if (ok)
-                  rv = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.res.ptr) +
-                                                       (e_nb * a.res.sn + (int64_t)e_dz * a.res.sd +
-                                                        (int64_t)ho * a.res.sh + (int64_t)wo * a.res.sw + co));
-                unpack8(rv, rr);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) tv[e] += rr[e];
-              }
-              if (use_acc) {
-                float o[8];
-                unpack8(ok ? *reinterpret_cast<const uint4*>(yp) : make_uint4(0, 0, 0, 0), o);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) tv[e] += o[e];
-              }
-              if (ok) *reinterpret_cast<uint4*>(yp) = Chunk<bf16>::pack(tv);
             }
+          asm volatile(
+              "s_nop 1\n\t"
+              "v_permlane32_swap_b32 %0, %4\n\tv_permlane32_swap_b32 %1, %5\n\t"
+              "v_permlane32_swap_b32 %2, %6\n\tv_permlane32_swap_b32 %3, %7\n\t"
+              "v_permlane32_swap_b32 %8, %12\n\tv_permlane32_swap_b32 %9, %13\n\t"
+              "v_permlane32_swap_b32 %10, %14\n\tv_permlane32_swap_b32 %11, %15"
+              : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+                "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]),
+                "+v"(v[15]));
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int cl = ns * 32 + q * 16;  // channel offset within the tile (lane half adds 8)
+            const bool ok = ok_w && e_n0 + cl + hf * 8 < a.cout;
+            float* tv = v + q * 8;
+            if (use_msk) {
+              float m[8];
+              unpack8(ok ? *reinterpret_cast<const uint4*>(mrow + cl) : make_uint4(0, 0, 0, 0), m);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) tv[e] = mask_apply(m[e], tv[e], mslope);
+            }
+            if (use_res) {
+              float rr[8];
+              unpack8(ok ? *reinterpret_cast<const uint4*>(rrow + cl) : make_uint4(0, 0, 0, 0), rr);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) tv[e] += rr[e];
+            }
+            if (use_acc) {
+              float o[8];
+              unpack8(ok ? *reinterpret_cast<const uint4*>(yrow + cl) : make_uint4(0, 0, 0, 0), o);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) tv[e] += o[e];
+            }
+            if (ok) *reinterpret_cast<uint4*>(yrow + cl) = Chunk<bf16>::pack(tv);
           }
 #pragma unroll
           for (int i = 0; i < 16; ++i) A[i] = 0.f;

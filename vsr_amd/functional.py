@@ -17,7 +17,7 @@ from ._native import ACT_NONE, ACT_PRELU, ACT_RELU, PRO_AFFINE, PRO_AFFINE_RELU,
 __all__ = [
     "pack_weight", "conv", "conv_wgrad", "to_view", "from_view", "relu_bwd", "add",
     "loss_fwd", "loss_bwd", "psnr", "ssim", "workspace", "LOSS_KINDS",
-    "bn_stats", "bn_finalize", "bn_fold_running", "bn_relu_bwd_reduce", "bn_relu_bwd_apply",
+    "bn_stats", "bn_finalize", "bn_fold_running", "bn_apply", "bn_relu_bwd_reduce", "bn_relu_bwd_apply",
     "duf_dynfilter_fwd", "duf_dynfilter_bwd",
     "subpixel_conv_weight", "subpixel_wgrad_fold", "prelu_wgrad", "prelu_bwd",
 ]
@@ -312,14 +312,23 @@ def bn_finalize(sums: torch.Tensor, count: float, gamma, beta, eps: float, momen
 
 
 def bn_fold_running(gamma, beta, running_mean, running_var, eps: float) -> torch.Tensor:
-    """eval mode -> (4, C): scale, shift (mean/invstd rows unused)."""
+    """eval mode -> (4, C): scale, shift, running mean, 1/sqrt(running var + eps)."""
     lib = _lib()
     c = running_mean.shape[0]
-    out = torch.zeros((4, c), dtype=torch.float32, device=running_mean.device)
+    out = torch.empty((4, c), dtype=torch.float32, device=running_mean.device)
     N.check(lib.vsrk_bn_fold_running(N.ptr(gamma), N.ptr(beta), running_mean.data_ptr(), running_var.data_ptr(),
-                                     float(eps), out[0].data_ptr(), out[1].data_ptr(), c,
-                                     N.stream_ptr(running_mean.device)), "bn_fold_running")
+                                     float(eps), out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(),
+                                     out[3].data_ptr(), c, N.stream_ptr(running_mean.device)), "bn_fold_running")
     return out
+
+
+def bn_apply(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, relu: bool, y: torch.Tensor) -> torch.Tensor:
+    """y = x * scale + shift [relu], per channel of channels-last views."""
+    lib = _lib()
+    xv, yv = N.t5(x), N.t5(y)
+    N.check(lib.vsrk_bn_apply(C.byref(xv), scale.data_ptr(), shift.data_ptr(), 1 if relu else 0, C.byref(yv),
+                              N.stream_ptr(x.device)), "bn_apply")
+    return y
 
 
 def bn_relu_bwd_reduce(x: torch.Tensor, dz: torch.Tensor, st: torch.Tensor) -> torch.Tensor:

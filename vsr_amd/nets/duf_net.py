@@ -96,7 +96,11 @@ class DUFNet(BaseNet):
     def _bn_forward(self, bn: nn.BatchNorm3d, x: torch.Tensor) -> torch.Tensor:
         """(4, C) = scale, shift, mean, invstd for the fused BN+ReLU prologue."""
         if not self.training:
-            return F.bn_fold_running(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
+            # running statistics; the backward (a gradient taken through an
+            # eval-mode net) then has no batch-statistics terms: count = inf
+            st = F.bn_fold_running(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
+            st.count = float("inf")
+            return st
         sums = F.bn_stats(x)
         count = x.shape[0] * x.shape[1] * x.shape[2] * x.shape[3]
         if self.bn_allreduce is not None:
@@ -119,7 +123,7 @@ class DUFNet(BaseNet):
         gb = self._grad_buffer(bn.bias)
         gw.copy_(red[1])
         gb.copy_(red[0])
-        if self.bn_allreduce is not None:
+        if self.bn_allreduce is not None and st.count != float("inf"):
             red = red.clone()
             self.bn_allreduce(red)
         F.bn_relu_bwd_apply(x, dz, st, bn.weight, red, st.count, dx, accumulate)
