@@ -40,3 +40,50 @@ def test_workspace_queries_are_host_only(native):
     y = Tensor5(None, 4, 16, 128, 128, 32, 0, 0, 0, 0, 1, 1)
     assert native.vsrk_conv_wgrad_workspace_size(C.byref(d), C.byref(x), C.byref(y)) > 0
     assert native.vsrk_conv_packed_elems(32, 64, 3, 3, 3, 0) == 27 * 128 * 64
+
+
+# ---- INTEGRATION.md's reference-side binding stub vs _native vs the header --
+DOC = HEADER.parent.parent / "INTEGRATION.md"
+_CTYPE = {"int32_t": "c_int", "int64_t": "c_long", "float": "c_float", "double": "c_double"}
+
+
+def _doc_structs():
+    import ctypes as C
+    text = DOC.read_text()
+    ns = {"C": C}
+    for name in ("Tensor5", "ConvDesc"):
+        m = re.search(rf"^class {name}\(C\.Structure\):.*?\]\n", text, re.S | re.M)
+        assert m, f"INTEGRATION.md has no {name} struct"
+        exec(m.group(0), ns)  # our own document's ctypes declaration
+    return ns["Tensor5"], ns["ConvDesc"]
+
+
+def _header_fields(struct):
+    body = re.search(rf"typedef struct {struct} \{{(.*?)\}} {struct};", HEADER.read_text(), re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    out = []
+    for decl in filter(None, (d.strip() for d in body.split(";"))):
+        ptr = "*" in decl
+        typ, names = decl.replace("*", " ").replace("const ", "").split(None, 1)
+        for n in (x.strip() for x in names.split(",")):
+            out.append((n, "c_void_p" if ptr else _CTYPE[typ]))
+    return out
+
+
+def _fields(cls):
+    return [(n, t.__name__) for n, t in cls._fields_]
+
+
+def test_integration_doc_structs_match_binding_and_header():
+    import ctypes as C
+    t5, cd = _doc_structs()
+    for doc, nat, hdr in ((t5, _native.Tensor5, "vsrk_tensor5"), (cd, _native.ConvDesc, "vsrk_conv_desc")):
+        assert _fields(doc) == _fields(nat), hdr
+        assert _fields(nat) == _header_fields(hdr), hdr
+        assert C.sizeof(doc) == C.sizeof(nat)
+
+
+def test_integration_doc_names_every_net():
+    text = DOC.read_text()
+    for net in ("EDSRNet", "DUFNet", "DRFNet", "DRFSISRNet"):
+        assert f"{net}" in text.split("## 2.")[0], net
