@@ -1,0 +1,176 @@
+"""Parity of the pointwise (1x1x1) bf16 conv kernels (conv_pw.hip) against
+torch fp64: forward / data gradient with every prologue and epilogue form the
+generators use, on channel- and depth-slice views of concat buffers (DUF's
+dense-unit layout, duf_net.py:195-214), output-channel chunks (the 256->512
+filter head, duf_net.py:40-44), and the weight gradient incl. cin/cout chunks,
+split tails and grid caps (several tiles / voxel ranges per workgroup).
+
+bf16 operands are rounded before the fp64 reference, so only accumulation
+order and the final store differ: forward max|d| <= 1.5e-2 max|ref|, weight
+gradient max|d| <= 1e-2 (1 + max|ref|)."""
+import pytest
+import torch
+import torch.nn.functional as Fn
+
+from vsr_amd import functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def _q(t):
+    return t.to(BF).double()
+
+
+def _ref1x1(x_cl, w, b):
+    """x (N,D,H,W,Ci) fp64, w (Co,Ci) -> (N,D,H,W,Co)."""
+    y = torch.einsum("ndhwc,oc->ndhwo", x_cl, w)
+    return y + b if b is not None else y
+
+
+@pytest.fixture(params=[0, 1, 3])
+def grid_cap(request):
+    F.set_grid_cap(request.param)
+    yield request.param
+    F.set_grid_cap(0)
+
+
+@pytest.mark.parametrize("c", [64, 80, 96, 128, 160, 192, 224, 256])
+def test_pw_forward_prologue_slices(c, grid_cap):
+    """BN-affine+ReLU prologue on a channel slice of a concat buffer, output into
+    a channel slice of another buffer, bias; tails of voxels (N*D*H*W not a
+    multiple of the tile)."""
+    g = torch.Generator().manual_seed(c)
+    n, d, h, w = 2, 3, 7, 19
+    big = torch.randn((n, d, h, w, c + 40), generator=g)
+    wt = torch.randn((c, c), generator=g) / c ** 0.5
+    b = torch.randn(c, generator=g)
+    sc = torch.rand(c, generator=g) + 0.5
+    sh = torch.randn(c, generator=g)
+    xin = torch.relu(_q(big[..., 8:8 + c]) * sc.double() + sh.double()).to(BF).double()
+    ref = _ref1x1(xin, _q(wt), b.double())
+    yb = torch.full((n, d, h, w, c + 24), 7.0, dtype=BF, device=DEV)
+    bigd = big.to(DEV, BF)
+    F.conv(bigd[..., 8:8 + c], F.pack_weight(wt.view(c, c, 1, 1, 1).to(DEV), 0, BF), yb[..., 16:16 + c],
+           (1, 1, 1), (0, 0, 0), bias=b.to(DEV), prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV),
+           pro_shift=sh.to(DEV))
+    y = yb[..., 16:16 + c].double().cpu()
+    err = (y - ref).abs().max().item()
+    assert err <= 1.5e-2 * ref.abs().max().item(), err
+    # the rest of the output buffer is untouched
+    assert (yb[..., :16] == 7.0).all() and (yb[..., 16 + c:] == 7.0).all()
+
+
+def test_pw_forward_depth_slice_head_chunks(grid_cap):
+    """256 -> 512 with ReLU prologue and ReLU act (filterNet.conv1) on a depth
+    slice (n stride != d*h*w*c): two 256-channel output chunks."""
+    g = torch.Generator().manual_seed(7)
+    n, D, h, w, ci, co = 3, 5, 6, 21, 256, 512
+    big = torch.randn((n, D, h, w, ci), generator=g)
+    x = big[:, 2:3]
+    wt = torch.randn((co, ci), generator=g) / ci ** 0.5
+    b = torch.randn(co, generator=g)
+    ref = torch.relu(_ref1x1(torch.relu(_q(x)), _q(wt), b.double()))
+    y = torch.empty((n, 1, h, w, co), dtype=BF, device=DEV)
+    F.conv(big.to(DEV, BF)[:, 2:3], F.pack_weight(wt.view(co, ci, 1, 1, 1).to(DEV), 0, BF), y, (1, 1, 1),
+           (0, 0, 0), bias=b.to(DEV), prologue=F.PRO_RELU, act=F.ACT_RELU)
+    err = (y.double().cpu() - ref).abs().max().item()
+    assert err <= 1.5e-2 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("combo", ["mask", "acc", "mask+acc"])
+@pytest.mark.parametrize("c", [128, 256])
+def test_pw_data_gradient_epilogues(c, combo, grid_cap):
+    """dgrad form (mode-1 packed weight, no prologue) with the ReLU mask of the
+    forward output and / or accumulation into an existing gradient."""
+    g = torch.Generator().manual_seed(c + 1)
+    n, d, h, w = 2, 2, 9, 13
+    gy = torch.randn((n, d, h, w, c), generator=g)
+    wt = torch.randn((c, c), generator=g) / c ** 0.5
+    mask = torch.randn((n, d, h, w, c), generator=g)
+    y0 = torch.randn((n, d, h, w, c), generator=g)
+    parts = set(combo.split("+"))
+    ref = torch.einsum("ndhwo,oc->ndhwc", _q(gy), _q(wt)) * 0.5
+    if "mask" in parts:
+        ref = torch.where(_q(mask) > 0, ref, torch.zeros_like(ref))
+    if "acc" in parts:
+        ref = ref + _q(y0)
+    yd = y0.to(DEV, BF)
+    F.conv(gy.to(DEV, BF), F.pack_weight(wt.view(c, c, 1, 1, 1).to(DEV), 1, BF), yd, (1, 1, 1), (0, 0, 0),
+           out_scale=0.5, mask=mask.to(DEV, BF) if "mask" in parts else None, accumulate="acc" in parts)
+    err = (yd.double().cpu() - ref).abs().max().item()
+    assert err <= 2 * 1.5e-2 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("ci,co", [(64, 64), (96, 96), (160, 160), (224, 224), (256, 256), (256, 512),
+                                   (512, 400), (48, 130), (80, 72)])
+@pytest.mark.parametrize("prologue", [False, True])
+def test_pw_weight_gradient(ci, co, prologue, grid_cap):
+    g = torch.Generator().manual_seed(ci * 3 + co)
+    n, D, h, w = 2, 4, 5, 23
+    big = torch.randn((n, D, h, w, ci + 16), generator=g)
+    x = big[:, 1:4, :, :, 8:8 + ci]  # depth and channel slice
+    gy = torch.randn((n, 3, h, w, co), generator=g)
+    sc = torch.rand(ci, generator=g) + 0.5
+    sh = torch.randn(ci, generator=g)
+    xin = _q(x)
+    if prologue:
+        xin = torch.relu(xin * sc.double() + sh.double()).to(BF).double()
+    ref_w = torch.einsum("ndhwo,ndhwc->oc", _q(gy), xin)
+    ref_b = _q(gy).sum((0, 1, 2, 3))
+    dw = torch.empty((co, ci, 1, 1, 1), device=DEV)
+    db = torch.empty(co, device=DEV)
+    kw = dict(prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV)) if prologue else {}
+    F.conv_wgrad(big.to(DEV, BF)[:, 1:4, :, :, 8:8 + ci], gy.to(DEV, BF), (1, 1, 1), (0, 0, 0), dw, db, **kw)
+    ew = (dw.view(co, ci).double().cpu() - ref_w).abs().max().item()
+    eb = (db.double().cpu() - ref_b).abs().max().item()
+    assert ew <= 1e-2 * (1 + ref_w.abs().max().item()), ew
+    assert eb <= 1e-2 * (1 + ref_b.abs().max().item()), eb
+
+
+def test_pw_weight_gradient_accumulate_scale_deterministic():
+    g = torch.Generator().manual_seed(99)
+    x = torch.randn((2, 7, 16, 40, 160), generator=g).to(DEV, BF)
+    gy = torch.randn((2, 7, 16, 40, 160), generator=g).to(DEV, BF)
+    outs = []
+    for _ in range(2):
+        dw = torch.ones((160, 160, 1, 1, 1), device=DEV)
+        db = torch.ones(160, device=DEV)
+        F.conv_wgrad(x, gy, (1, 1, 1), (0, 0, 0), dw, db, dy_scale=0.25, accumulate=True)
+        outs.append((dw, db))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ref = torch.einsum("ndhwo,ndhwc->oc", gy.double(), x.double()).cpu() * 0.25 + 1
+    assert (outs[0][0].view(160, 160).double().cpu() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("c", [64, 192])
+def test_pw_matches_tile_kernels(c):
+    """pointwise kernels == the tile kernels (path "pw" off) on the same bf16
+    operands, forward with prologue, data gradient and weight gradient."""
+    g = torch.Generator().manual_seed(5 + c)
+    x = torch.randn((2, 3, 11, 33, c), generator=g).to(DEV, BF)
+    gy = torch.randn((2, 3, 11, 33, c), generator=g).to(DEV, BF)
+    wt = (torch.randn((c, c, 1, 1, 1), generator=g) / c ** 0.5).to(DEV)
+    b = torch.randn(c, generator=g).to(DEV)
+    sc = (torch.rand(c, generator=g) + 0.5).to(DEV)
+    sh = torch.randn(c, generator=g).to(DEV)
+    res = []
+    for mode in (1, 0):
+        F.set_conv_path("pw", mode)
+        try:
+            y = torch.empty_like(x)
+            F.conv(x, F.pack_weight(wt, 0, BF), y, (1, 1, 1), (0, 0, 0), bias=b, prologue=F.PRO_AFFINE_RELU,
+                   pro_scale=sc, pro_shift=sh)
+            dx = torch.empty_like(x)
+            F.conv(gy, F.pack_weight(wt, 1, BF), dx, (1, 1, 1), (0, 0, 0))
+            dw = torch.empty((c, c, 1, 1, 1), device=DEV)
+            db = torch.empty(c, device=DEV)
+            F.conv_wgrad(x, gy, (1, 1, 1), (0, 0, 0), dw, db, prologue=F.PRO_AFFINE_RELU, pro_scale=sc,
+                         pro_shift=sh)
+            res.append((y.float(), dx.float(), dw, db))
+        finally:
+            F.set_conv_path("pw", -1)
+    for a_, b_ in zip(res[0], res[1]):
+        # bf16 outputs may differ by one rounding step; fp32 gradients by summation order
+        assert (a_ - b_).abs().max().item() <= 1e-2 * (1 + b_.abs().max().item())

@@ -18,6 +18,8 @@ CASES = {
     "duf64": (64, 7, 128, 128, 64, 32, (3, 3, 3), (1, 1, 1)),
     "duf224v": (64, 7, 128, 128, 224, 32, (3, 3, 3), (0, 1, 1)),
     "duf1x1x1": (64, 7, 128, 128, 128, 128, (1, 1, 1), (0, 0, 0)),
+    "duf1x1x1_224": (64, 3, 128, 128, 224, 224, (1, 1, 1), (0, 0, 0)),
+    "duf1x1x1_64": (64, 7, 128, 128, 64, 64, (1, 1, 1), (0, 0, 0)),
     # EDSR tail conv F -> 1 at HR (thin-channel kernels: fwd = thin-out, dgrad = thin-in)
     "tail": (64, 1, 512, 512, 64, 1, (1, 3, 3), (0, 1, 1)),
     "head": (64, 1, 128, 128, 1, 64, (1, 3, 3), (0, 1, 1)),
@@ -62,13 +64,17 @@ def main():
     esz = {torch.bfloat16: 2, torch.float32: 4}
     nbytes = {"fwd": x.numel() // x.shape[-1] * (ci * 2) + y.numel() * esz[y.dtype],
               "dgrad": gy.numel() // gy.shape[-1] * (co * 2) + dx.numel() * esz[dx.dtype],
+              "fwdpro": x.numel() // x.shape[-1] * (ci * 2) + y.numel() * esz[y.dtype],
               "wgrad": x.numel() // x.shape[-1] * (ci * 2) + gy.numel() // gy.shape[-1] * (co * 2)}
     dw = torch.empty((co, ci, *k), device=dev)
     db = torch.empty(co, device=dev)
     wp = F.pack_weight(wt, 0, dt)
+    psc = torch.rand(ci, generator=g).to(dev) + 0.5
+    psh = torch.randn(ci, generator=g).to(dev)
     flop = 2.0 * n * do * h * w * co * ci * k[0] * k[1] * k[2]
     cases = {
         "fwd": lambda: F.conv(x, wp, y, k, pad, bias=b),
+        "fwdpro": lambda: F.conv(x, wp, y, k, pad, bias=b, prologue=F.PRO_AFFINE_RELU, pro_scale=psc, pro_shift=psh),
         "res": lambda: F.conv(x, wp, y, k, pad, bias=b, out_scale=0.1, residual=res),
         "wgrad": lambda: F.conv_wgrad(x, gy, k, pad, dw, db),
         "dgrad": lambda: F.conv(gy, wp1, dx, k, dpad),

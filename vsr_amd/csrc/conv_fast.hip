@@ -44,7 +44,8 @@ extern "C" int vsrk_conv_set_path(const char* path, int32_t mode) {
   else if (p == "thin") vsrk_g_thin_mode = mode;
   else if (p == "wgrad_fast") vsrk_g_wgrad_fast_mode = mode;
   else if (p == "k3") vsrk_g_k3_mode = mode;
-  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, k3, thin, wgrad_fast)", path);
+  else if (p == "pw") vsrk_g_pw_mode = mode;
+  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, k3, pw, thin, wgrad_fast)", path);
   return VSRK_OK;
 }
 

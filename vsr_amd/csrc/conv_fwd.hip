@@ -511,6 +511,8 @@ extern "C" int vsrk_conv_fwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, con
   const int NT = y->c <= 32 ? 32 : ((y->c <= 64 || d->kh == 3) ? 64 : 128);
   a.ntn = ceil_div(y->c, NT);
   hipStream_t s = (hipStream_t)stream;
+  const int pw = vsrk_conv_fwd_pw(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s);
+  if (pw != 0) return pw > 0 ? VSRK_OK : -pw;
   const int thin = vsrk_conv_fwd_thin(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s);
   if (thin != 0) return thin > 0 ? VSRK_OK : -thin;
   const int fast = vsrk_conv_fwd_fast(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s);

@@ -1,0 +1,675 @@
+// Pointwise (1x1x1) convolution on CDNA4 for bf16 channels-last activations:
+// forward / data-gradient (pw_fwd) and weight gradient (pw_wgrad).
+//
+// DUF's dense-unit bottlenecks (BN3d-ReLU-Conv1x1x1, duf_net.py:198-200,
+// cin = cout = 64..224 at up to 7 x 128 x 128 voxels per sample) and its
+// 256-channel heads (duf_net.py:40-49) move (cin + cout) * 2 bytes per voxel
+// for 2 * cin * cout flops: <= 256 flop/B at cin = cout <= 256, under the
+// MI355X ridge (2.5 PF / 8 TB/s ~ 312 flop/B).  They are HBM-bound, so the
+// design goal is ONE pass over x and y at full HBM rate (the 3x3 tile kernels
+// re-read x once per 128-channel output tile and stage it through LDS with a
+// barrier per tile):
+//
+//  * pw_fwd: the weight chunk (<= 256 x 256 bf16 = 128 KiB) is staged into LDS
+//    once per workgroup.  Each wave then streams its own 32*M-voxel tiles
+//    straight from HBM into registers as the MFMA B operand (x^T: lane l holds
+//    voxel l&31, 8 channels), applies the BatchNorm+ReLU prologue in
+//    registers, runs all output-channel blocks against the resident weights
+//    (A operand, one conflict-free ds_read_b128 per MFMA) and stores: no
+//    barrier after the weight load, the next tile's loads in flight during
+//    the current tile's MFMAs and stores.
+//  * pw_wgrad: dW = dY^T X reduces over voxels.  Each workgroup owns a
+//    contiguous voxel range and a (cout chunk x cin chunk) of <= 256 x 256,
+//    stages 64 voxels of dY and X per step (register-staged double buffer,
+//    planar 64-byte rows read transposed with ds_read_b64_tr_b16), and writes
+//    one fp32 partial slab; pw_wgrad_reduce sums the slabs in split order
+//    (deterministic).  One pass over dY and X per cin/cout chunk.
+#include <algorithm>
+#include <cstdlib>
+#include "conv_common.h"
+
+int vsrk_g_pw_mode = -1;  // -1: from VSRK_CONV_PW (default on), 0 off, 1 on
+
+namespace {
+using namespace vsrk_conv;
+
+constexpr int PW_THR = 256;  // 4 waves, one per SIMD
+constexpr int PW_KP = 64;    // wgrad voxels per stage
+
+static bool pw_enabled() {
+  if (vsrk_g_pw_mode < 0) {
+    const char* e = getenv("VSRK_CONV_PW");
+    vsrk_g_pw_mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  return vsrk_g_pw_mode == 1;
+}
+
+static int pw_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+// Voxel v of a view whose (d, h, w) block is dense (sd = h*sh, sh = w*sw):
+// element offset n*sn + r*sw with n = v / dhw, r = v % dhw.
+__device__ __forceinline__ int64_t vox_off(int64_t v, int dhw, int64_t sn, int64_t sw) {
+  const int n = (int)(v / dhw);
+  const int r = (int)(v - (int64_t)n * dhw);
+  return n * sn + (int64_t)r * sw;
+}
+
+__device__ __forceinline__ uint4 bf16x8_affine(uint4 v, const float4& s0, const float4& s1, const float4& h0,
+                                               const float4& h1, bool relu) {
+  float f[8];
+  Chunk<bf16>::unpack(v, f);
+  const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float t = fmaf(f[e], sc[e], sh[e]);
+    f[e] = relu ? fmaxf(t, 0.f) : t;
+  }
+  return Chunk<bf16>::pack(f);
+}
+
+struct PwArgs {
+  const bf16* x;
+  bf16* y;
+  const bf16* msk;
+  const bf16* w;  // packed [round_up(cout,128)][ci_pad] (vsrk_conv_pack_weight)
+  const float* bias;
+  const float* pro_scale;
+  const float* pro_shift;
+  const float* mask_slope;
+  int64_t xsn, xsw, ysn, ysw, msn, msw;
+  int64_t nvox;
+  int dhw;
+  int cin, cout, ci_pad, co_rows;
+  int prologue, act, accumulate, has_mask;
+  float out_scale;
+  int ntiles;  // tiles of 32*M voxels
+};
+
+// ---------------------------------------------------------------------------
+// forward / data gradient: y[v][co] = epi(sum_ci W[co][ci] * pro(x[v][ci]))
+// NCB output blocks of 32 channels per workgroup (blockIdx.y picks the chunk),
+// KS = 2*NCB k-steps of 16 input channels (cin_pad == 32*NCB), M tiles of 32
+// voxels per wave step.
+// ---------------------------------------------------------------------------
+template <int NCB, int M, bool PRO, bool EIN>
+__global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
+  constexpr int KS = 2 * NCB;
+  constexpr int COP = 32 * NCB;
+  constexpr int CIP = 16 * KS;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* lw = lds;                                        // [KS][2][COP] x 16 B
+  float* lsc = reinterpret_cast<float*>(lds + KS * 2 * COP * 16);  // [CIP]
+  float* lsh = lsc + CIP;                                // [CIP]
+  float* lb = lsh + CIP;                                 // [COP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, col = lane & 31;
+  const int co0 = blockIdx.y * COP;
+
+  for (int i = tid; i < KS * 2 * COP; i += PW_THR) {
+    const int co = i % COP, t = i / COP, h = t & 1, s = t >> 1;
+    const int ci = 16 * s + 8 * h;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (ci < a.ci_pad && co0 + co < a.co_rows)
+      v = *reinterpret_cast<const uint4*>(a.w + (int64_t)(co0 + co) * a.ci_pad + ci);
+    *reinterpret_cast<uint4*>(lw + i * 16) = v;
+  }
+  if (PRO) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, CIP, tid, PW_THR);
+  for (int i = tid; i < COP; i += PW_THR) lb[i] = (a.bias && co0 + i < a.cout) ? a.bias[co0 + i] : 0.f;
+  __syncthreads();
+
+  const bool relu_in = (a.prologue & VSRK_PRO_RELU) != 0;
+  const float mslope = a.mask_slope ? *a.mask_slope : 0.f;
+  const int nwaves = gridDim.x * (PW_THR / 64);
+
+  auto load = [&](int tile, uint4 (&b)[M][KS]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int64_t v = ((int64_t)tile * M + m) * 32 + col;
+      const bool ok = v < a.nvox;
+      const bf16* p = a.x + (ok ? vox_off(v, a.dhw, a.xsn, a.xsw) : 0) + 8 * hf;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const bool cok = ok && 16 * s + 8 * hf < a.cin;
+        b[m][s] = cok ? *reinterpret_cast<const uint4*>(p + 16 * s) : make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+
+  uint4 bc[M][KS];
+  int t = blockIdx.x * (PW_THR / 64) + wave;
+  if (t < a.ntiles) load(t, bc);
+  while (t < a.ntiles) {
+    const int tn = t + nwaves;
+    // epilogue inputs of this tile first, then the next tile's operands: the
+    // epilogue's wait (vmcnt) then leaves the prefetch in flight
+    uint2 ein[EIN ? M : 1][NCB][4];
+    constexpr bool need_in = EIN;  // mask and/or accumulate
+    if constexpr (EIN) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int64_t v = ((int64_t)t * M + m) * 32 + col;
+        const bool ok = v < a.nvox;
+        const bf16* src = a.has_mask ? a.msk : a.y;
+        const int64_t off = ok ? (a.has_mask ? vox_off(v, a.dhw, a.msn, a.msw) : vox_off(v, a.dhw, a.ysn, a.ysw)) : 0;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int gco = co0 + cb * 32 + 8 * j + 4 * hf;
+            ein[m][cb][j] = (ok && gco < a.cout) ? *reinterpret_cast<const uint2*>(src + off + gco) : make_uint2(0, 0);
+          }
+      }
+    }
+    uint4 bn[M][KS];
+    if (tn < a.ntiles) load(tn, bn);
+
+    f32x16 acc[M][NCB];
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[m][cb][i] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (PRO) {
+        const int c = 16 * s + 8 * hf;
+        const float4 s0 = *reinterpret_cast<const float4*>(lsc + c), s1 = *reinterpret_cast<const float4*>(lsc + c + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(lsh + c), h1 = *reinterpret_cast<const float4*>(lsh + c + 4);
+#pragma unroll
+        for (int m = 0; m < M; ++m) bc[m][s] = bf16x8_affine(bc[m][s], s0, s1, h0, h1, relu_in);
+      }
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        const uint4 af = *reinterpret_cast<const uint4*>(lw + ((s * 2 + hf) * COP + cb * 32 + col) * 16);
+#pragma unroll
+        for (int m = 0; m < M; ++m) mma<bf16>(acc[m][cb], af, bc[m][s]);
+      }
+      // keep the scheduler from hoisting every k-step's weight reads (register pressure)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // epilogue: lane holds voxel col, channels cb*32 + 8j + 4hf + (0..3)
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int64_t v = ((int64_t)t * M + m) * 32 + col;
+      if (v < a.nvox) {
+        bf16* yp = a.y + vox_off(v, a.dhw, a.ysn, a.ysw);
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int co = cb * 32 + 8 * j + 4 * hf;
+            if (co0 + co < a.cout) {
+              const float4 bb = *reinterpret_cast<const float4*>(lb + co);
+              float o[4] = {acc[m][cb][4 * j] + bb.x, acc[m][cb][4 * j + 1] + bb.y, acc[m][cb][4 * j + 2] + bb.z,
+                            acc[m][cb][4 * j + 3] + bb.w};
+              float e4[4] = {0.f, 0.f, 0.f, 0.f};
+              if constexpr (EIN) unpack_pk<bf16>(ein[m][cb][j], e4);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                float r = act_apply(a.act, o[e] * a.out_scale, 0.f);
+                if (a.has_mask) r = mask_apply(e4[e], r, mslope);
+                o[e] = r;
+              }
+              if (a.accumulate) {
+                if (a.has_mask) {
+                  float y4[4];
+                  unpack_pk<bf16>(*reinterpret_cast<const uint2*>(yp + co0 + co), y4);
+#pragma unroll
+                  for (int e = 0; e < 4; ++e) o[e] += y4[e];
+                } else {
+#pragma unroll
+                  for (int e = 0; e < 4; ++e) o[e] += e4[e];
+                }
+              }
+              *reinterpret_cast<uint2*>(yp + co0 + co) = pack_pk<bf16, uint2>(o);
+            }
+          }
+        }
+      }
+    }
+    if (tn < a.ntiles) {
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) bc[m][s] = bn[m][s];
+    }
+    t = tn;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient
+// ---------------------------------------------------------------------------
+struct PwWArgs {
+  const bf16* x;
+  const bf16* dy;
+  const float* pro_scale;
+  const float* pro_shift;
+  float* ws;
+  int64_t xsn, xsw, dsn, dsw;
+  int64_t nvox, vox_per_split;
+  int dhw;
+  int cin, cout, prologue;
+  int ncit;                  // ci blocks in this launch's chunks (<= 4*NCIW)
+  int ci_chunks, nchunks;    // blockIdx.y = co_chunk * ci_chunks + ci_chunk
+  int slab;                  // floats per (split, chunk): 32*NCO * 32*ncit + 32*NCO
+  int want_bias;
+};
+
+// NCO dY channel blocks per chunk; wave w owns X blocks w, w+4 (NCIW of them).
+template <int NCO, int NCIW>
+__global__ __launch_bounds__(PW_THR, 1) void pw_wgrad_kernel(PwWArgs a) {
+  constexpr int PLMAX = NCO + 4 * NCIW;  // 32-channel planes per stage (max)
+  constexpr int PSZ = PW_KP * 64;        // bytes per plane: 64 voxel rows of 32 bf16
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int PL = NCO + a.ncit;
+  const int NCH = PL * 4;            // 16-byte chunks per voxel
+  const int split = blockIdx.x, chunk = blockIdx.y;
+  const int co_chunk = chunk / a.ci_chunks, ci_chunk = chunk - co_chunk * a.ci_chunks;
+  const int co0 = co_chunk * 32 * NCO, ci0 = ci_chunk * 32 * a.ncit;
+  const int64_t vbeg = (int64_t)split * a.vox_per_split;
+  const int64_t vend = std::min<int64_t>(a.nvox, vbeg + a.vox_per_split);
+  const int nst = vend > vbeg ? (int)((vend - vbeg + PW_KP - 1) / PW_KP) : 0;
+  const bool relu_in = (a.prologue & VSRK_PRO_RELU) != 0;
+  const bool aff = (a.prologue & VSRK_PRO_AFFINE) != 0;
+  const bool do_bias = a.want_bias && ci_chunk == 0 && wave == 0;
+
+  // per-thread chunk roles (PL chunks per thread per stage)
+  uint4 rg[PLMAX];
+  auto issue = [&](int st) __attribute__((always_inline)) {
+    const int64_t v0 = vbeg + (int64_t)st * PW_KP;
+    const int n0 = (int)(v0 / a.dhw);
+    const int r0 = (int)(v0 - (int64_t)n0 * a.dhw);
+#pragma unroll
+    for (int k = 0; k < PLMAX; ++k) {
+      if (k < PL) {
+        const int i = tid + k * PW_THR;
+        const int vox = i / NCH, within = i - vox * NCH;
+        const int plane = within >> 2, q = within & 3;
+        int n = n0, r = r0 + vox;
+        while (r >= a.dhw) { r -= a.dhw; ++n; }
+        const bool vok = v0 + vox < vend;
+        uint4 val = make_uint4(0, 0, 0, 0);
+        if (plane < NCO) {
+          const int c = co0 + plane * 32 + q * 8;
+          if (vok && c < a.cout) val = *reinterpret_cast<const uint4*>(a.dy + n * a.dsn + (int64_t)r * a.dsw + c);
+        } else {
+          const int c = ci0 + (plane - NCO) * 32 + q * 8;
+          if (vok && c < a.cin) val = *reinterpret_cast<const uint4*>(a.x + n * a.xsn + (int64_t)r * a.xsw + c);
+        }
+        rg[k] = val;
+      }
+    }
+  };
+  auto commit = [&](int buf) __attribute__((always_inline)) {
+    char* base = lds + buf * (PLMAX * PSZ);
+#pragma unroll
+    for (int k = 0; k < PLMAX; ++k) {
+      if (k < PL) {
+        const int i = tid + k * PW_THR;
+        const int vox = i / NCH, within = i - vox * NCH;
+        const int plane = within >> 2, q = within & 3;
+        *reinterpret_cast<uint4*>(base + plane * PSZ + vox * 64 + q * 16) = rg[k];
+      }
+    }
+  };
+
+  // prologue scale/shift of the lane's X channel in each owned block
+  float psc[NCIW], psh[NCIW];
+#pragma unroll
+  for (int b = 0; b < NCIW; ++b) {
+    const int c = ci0 + (wave + 4 * b) * 32 + (lane & 31);
+    const bool ok = c < a.cin;
+    psc[b] = ok ? (aff ? a.pro_scale[c] : 1.f) : 0.f;
+    psh[b] = ok ? (aff ? a.pro_shift[c] : 0.f) : 0.f;
+  }
+
+  f32x16 acc[NCO][NCIW];
+#pragma unroll
+  for (int i = 0; i < NCO; ++i)
+#pragma unroll
+    for (int b = 0; b < NCIW; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][b][e] = 0.f;
+  float bsum[NCO];
+#pragma unroll
+  for (int i = 0; i < NCO; ++i) bsum[i] = 0.f;
+
+  // ds_read_b64_tr_b16: group g = lane>>4 reads a 4-voxel x 16-channel block;
+  // lane 4q+p addresses voxel row q, channels 4p..4p+3, and receives channel
+  // lane&15 of the group's 16: lane l ends up with channel l&31 of the plane
+  // for voxels 8*(l>>5) .. +7 of the k-step.
+  const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  const int colb = ((g & 1) * 16 + 4 * p) * 2;
+  const int rowk = 8 * (g >> 1) + q;
+
+  if (nst > 0) {
+    issue(0);
+    commit(0);
+    __syncthreads();
+  }
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) issue(st + 1);
+    const char* base = lds + (st & 1) * (PLMAX * PSZ);
+#pragma unroll
+    for (int kk = 0; kk < PW_KP / 16; ++kk) {
+      const int row = kk * 16 + rowk;
+      bf16x8 bfr[NCIW];
+#pragma unroll
+      for (int b = 0; b < NCIW; ++b) {
+        const int blk = wave + 4 * b;
+        if (blk < a.ncit) {
+          const char* px = base + (NCO + blk) * PSZ + row * 64 + colb;
+          const v4i16 x0 = ds_read_tr(px), x1 = ds_read_tr(px + 4 * 64);
+          uint4 xv = __builtin_bit_cast(uint4, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+          if (a.prologue) {
+            float f[8];
+            Chunk<bf16>::unpack(xv, f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float tt = fmaf(f[e], psc[b], psh[b]);
+              f[e] = relu_in ? fmaxf(tt, 0.f) : tt;
+            }
+            xv = Chunk<bf16>::pack(f);
+          }
+          bfr[b] = __builtin_bit_cast(bf16x8, xv);
+        }
+      }
+#pragma unroll
+      for (int cb = 0; cb < NCO; ++cb) {
+        const char* py = base + cb * PSZ + row * 64 + colb;
+        const v4i16 y0 = ds_read_tr(py), y1 = ds_read_tr(py + 4 * 64);
+        const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7));
+        if (do_bias) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bsum[cb] += (float)af[e];
+        }
+#pragma unroll
+        for (int b = 0; b < NCIW; ++b)
+          if (wave + 4 * b < a.ncit)
+            acc[cb][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[b], acc[cb][b], 0, 0, 0);
+      }
+    }
+    if (st + 1 < nst) commit((st + 1) & 1);
+    __syncthreads();
+  }
+
+  // slab: [co (32*NCO)][ci (32*ncit)] then dbias[32*NCO]
+  const int cic = 32 * a.ncit;
+  float* out = a.ws + ((int64_t)split * a.nchunks + chunk) * a.slab;
+  const int hf = lane >> 5, col = lane & 31;
+#pragma unroll
+  for (int cb = 0; cb < NCO; ++cb)
+#pragma unroll
+    for (int b = 0; b < NCIW; ++b) {
+      const int blk = wave + 4 * b;
+      if (blk < a.ncit) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int co = cb * 32 + 8 * (e >> 2) + 4 * hf + (e & 3);
+          out[co * cic + blk * 32 + col] = acc[cb][b][e];
+        }
+      }
+    }
+  if (a.want_bias && ci_chunk == 0 && wave == 0) {
+#pragma unroll
+    for (int cb = 0; cb < NCO; ++cb) {
+      const float tot = bsum[cb] + __shfl_xor(bsum[cb], 32);
+      if (hf == 0) out[32 * NCO * cic + cb * 32 + col] = tot;
+    }
+  }
+}
+
+// dw[co][ci] (torch layout of a 1x1x1 weight, fp32) [+]= scale * sum over
+// splits of the slabs, in split order; then dbias.
+__global__ __launch_bounds__(256) void pw_wgrad_reduce(const float* __restrict__ ws, float* __restrict__ dw,
+                                                      float* __restrict__ db, int nsplit, int nchunks, int slab,
+                                                      int cout, int cin, int cop, int cic, int ci_chunks,
+                                                      float scale, int accumulate) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nw = (int64_t)cout * cin;
+  if (idx >= nw + (db ? cout : 0)) return;
+  int co, ci;
+  const float* p;
+  const int64_t sstride = (int64_t)nchunks * slab;
+  if (idx < nw) {
+    co = (int)(idx / cin);
+    ci = (int)(idx - (int64_t)co * cin);
+    const int chunk = (co / cop) * ci_chunks + ci / cic;
+    p = ws + (int64_t)chunk * slab + (int64_t)(co % cop) * cic + (ci % cic);
+  } else {
+    co = (int)(idx - nw);
+    ci = 0;
+    const int chunk = (co / cop) * ci_chunks;
+    p = ws + (int64_t)chunk * slab + (int64_t)cop * cic + (co % cop);
+  }
+  float s = 0.f;
+  for (int k = 0; k < nsplit; ++k) s += p[k * sstride];
+  s *= scale;
+  if (idx < nw) {
+    float* d = dw + idx;
+    *d = accumulate ? *d + s : s;
+  } else {
+    db[co] = accumulate ? db[co] + s : s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static bool dhw_dense(const vsrk_tensor5* t) {
+  return t->shuffle <= 1 && t->sw >= t->c && (t->h == 1 || t->sh == (int64_t)t->w * t->sw) &&
+         (t->d == 1 || t->sd == (int64_t)t->h * t->sh);
+}
+
+template <int NCB, int M>
+static void launch_fwd(const PwArgs& a, int nchunk, bool pro, hipStream_t s) {
+  constexpr int KS = 2 * NCB, COP = 32 * NCB, CIP = 16 * KS;
+  const size_t lds = (size_t)KS * 2 * COP * 16 + (2 * CIP + COP) * sizeof(float);
+  const int64_t waves = (a.ntiles + 0);
+  int grid = (int)std::min<int64_t>(pw_num_cus(), ceil_div64(waves, PW_THR / 64));
+  if (vsrk_g_grid_cap > 0) grid = std::min(grid, vsrk_g_grid_cap);
+  grid = std::max(grid, 1);
+  const bool ein = a.has_mask || a.accumulate;
+  auto kern = pro ? (ein ? pw_fwd_kernel<NCB, M, true, true> : pw_fwd_kernel<NCB, M, true, false>)
+                  : (ein ? pw_fwd_kernel<NCB, M, false, true> : pw_fwd_kernel<NCB, M, false, false>);
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  kern<<<dim3(grid, nchunk), PW_THR, lds, s>>>(a);
+}
+
+// tiles of 32*M voxels, M chosen so one wave step loads ~16 KiB
+template <int NCB>
+constexpr int pw_m() { return NCB <= 2 ? 4 : (NCB <= 4 ? 2 : 1); }
+
+}  // namespace
+
+// 1 = launched, 0 = not eligible (caller uses the tile kernels), <0 = -status.
+int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                     const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
+                     const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s) {
+  if (!pw_enabled()) return 0;
+  if (x->dtype != VSRK_BF16 || y->dtype != VSRK_BF16) return 0;
+  if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->pd || d->ph || d->pw) return 0;
+  if (residual || d->act == VSRK_ACT_PRELU || d->bias_perm_r > 1) return 0;
+  if (x->n != y->n || x->d != y->d || x->h != y->h || x->w != y->w) return 0;
+  if (!dhw_dense(x) || !dhw_dense(y) || (mask && (!dhw_dense(mask) || mask->dtype != VSRK_BF16))) return 0;
+  if (mask && (mask->n != y->n || mask->d != y->d || mask->h != y->h || mask->w != y->w || mask->c != y->c)) return 0;
+  if (x->c % 8 || y->c % 4 || !chunk_ok(x, 2)) return 0;
+  if (((uintptr_t)y->ptr) % 8 || y->sn % 4 || y->sw % 4) return 0;
+  if (mask && (((uintptr_t)mask->ptr) % 8 || mask->sn % 4 || mask->sw % 4)) return 0;
+  const int cip = round_up(x->c, 32);
+  const int ncb = cip / 32;  // square kernels: COP = CIP
+  if (ncb < 2 || ncb > 8) return 0;
+  const int cop_total = round_up(y->c, 32);
+  if (cop_total % cip != 0) return 0;  // output handled in chunks of CIP channels
+  const int nchunk = cop_total / cip;
+  PwArgs a;
+  a.x = (const bf16*)x->ptr;
+  a.y = (bf16*)y->ptr;
+  a.msk = mask ? (const bf16*)mask->ptr : nullptr;
+  a.w = (const bf16*)w_packed;
+  a.bias = bias;
+  a.pro_scale = pro_scale;
+  a.pro_shift = pro_shift;
+  a.mask_slope = d->mask_slope;
+  a.xsn = x->sn; a.xsw = x->sw;
+  a.ysn = y->sn; a.ysw = y->sw;
+  a.msn = mask ? mask->sn : 0;
+  a.msw = mask ? mask->sw : 0;
+  a.dhw = x->d * x->h * x->w;
+  a.nvox = (int64_t)x->n * a.dhw;
+  a.cin = x->c;
+  a.cout = y->c;
+  a.ci_pad = cip;
+  a.co_rows = round_up(y->c, 128);
+  a.prologue = d->prologue;
+  a.act = d->act;
+  a.accumulate = d->accumulate;
+  a.has_mask = mask != nullptr;
+  a.out_scale = d->out_scale;
+  if (a.nvox == 0) return 1;
+  const bool pro = d->prologue != VSRK_PRO_NONE;
+  switch (ncb) {
+#define PW_CASE(N)                                                     \
+  case N:                                                              \
+    a.ntiles = (int)ceil_div64(a.nvox, 32 * pw_m<N>());                \
+    launch_fwd<N, pw_m<N>()>(a, nchunk, pro, s);                       \
+    break;
+    PW_CASE(2) PW_CASE(3) PW_CASE(4) PW_CASE(5) PW_CASE(6) PW_CASE(7) PW_CASE(8)
+#undef PW_CASE
+    default:
+      return 0;
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    vsrk_set_error("conv_fwd_pw: launch failed: %s", hipGetErrorString(e));
+    return -VSRK_ERR_LAUNCH;
+  }
+  return 1;
+}
+
+namespace {
+struct PwWPlan {
+  bool ok;
+  int nco, ncit, ncoiw, ci_chunks, co_chunks, nchunks, nsplit, slab;
+  int64_t vps;
+  size_t ws_bytes;
+};
+
+PwWPlan pw_wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk_tensor5* dy) {
+  PwWPlan p{};
+  p.ok = false;
+  if (!pw_enabled()) return p;
+  if (x->dtype != VSRK_BF16 || dy->dtype != VSRK_BF16) return p;
+  if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->pd || d->ph || d->pw) return p;
+  if (x->n != dy->n || x->d != dy->d || x->h != dy->h || x->w != dy->w) return p;
+  if (!dhw_dense(x) || !dhw_dense(dy) || !chunk_ok(x, 2) || !chunk_ok(dy, 2)) return p;
+  if (x->c % 8 || dy->c % 8) return p;
+  const int cob = ceil_div(dy->c, 32), cib = ceil_div(x->c, 32);
+  p.nco = std::min(cob, 8);
+  p.co_chunks = ceil_div(cob, p.nco);
+  p.ncit = std::min(cib, 8);
+  p.ci_chunks = ceil_div(cib, p.ncit);
+  if (p.nco < 2) return p;
+  p.ncoiw = ceil_div(p.ncit, 4);
+  p.nchunks = p.co_chunks * p.ci_chunks;
+  const int64_t nvox = (int64_t)x->n * x->d * x->h * x->w;
+  const int64_t steps = std::max<int64_t>(1, ceil_div64(nvox, PW_KP));
+  int want = std::max(1, pw_num_cus() / p.nchunks);
+  if (vsrk_g_grid_cap > 0) want = std::max(1, vsrk_g_grid_cap / p.nchunks);
+  want = (int)std::min<int64_t>(want, steps);
+  p.vps = ceil_div64(steps, want) * PW_KP;
+  p.nsplit = (int)std::max<int64_t>(1, ceil_div64(nvox, p.vps));
+  p.slab = 32 * p.nco * 32 * p.ncit + 32 * p.nco;
+  p.ws_bytes = (size_t)p.nsplit * p.nchunks * p.slab * sizeof(float);
+  p.ok = true;
+  return p;
+}
+
+template <int NCO, int NCIW>
+void launch_wgrad_pw(const PwWArgs& a, int nsplit, hipStream_t s) {
+  const size_t lds = (size_t)2 * (NCO + 4 * NCIW) * PW_KP * 64;
+  auto kern = pw_wgrad_kernel<NCO, NCIW>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  kern<<<dim3(nsplit, a.nchunks), PW_THR, lds, s>>>(a);
+}
+}  // namespace
+
+size_t vsrk_conv_wgrad_pw_workspace(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk_tensor5* dy) {
+  const PwWPlan p = pw_wgrad_plan(d, x, dy);
+  return p.ok ? p.ws_bytes : 0;
+}
+
+// 1 = launched (kernel + reduce), 0 = not eligible, <0 = -status.
+int vsrk_conv_wgrad_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk_tensor5* dy,
+                       const float* pro_scale, const float* pro_shift, float dy_scale, int32_t perm_r, float* dw,
+                       float* dbias, int32_t accumulate, void* workspace, size_t workspace_bytes, hipStream_t s) {
+  if (perm_r > 1) return 0;
+  const PwWPlan p = pw_wgrad_plan(d, x, dy);
+  if (!p.ok) return 0;
+  if (!workspace || workspace_bytes < p.ws_bytes) {
+    vsrk_set_error("conv_wgrad: workspace %zu < %zu bytes", workspace_bytes, p.ws_bytes);
+    return -VSRK_ERR_INVALID;
+  }
+  PwWArgs a;
+  a.x = (const bf16*)x->ptr;
+  a.dy = (const bf16*)dy->ptr;
+  a.pro_scale = pro_scale;
+  a.pro_shift = pro_shift;
+  a.ws = (float*)workspace;
+  a.xsn = x->sn; a.xsw = x->sw;
+  a.dsn = dy->sn; a.dsw = dy->sw;
+  a.nvox = (int64_t)x->n * x->d * x->h * x->w;
+  a.vox_per_split = p.vps;
+  a.dhw = x->d * x->h * x->w;
+  a.cin = x->c;
+  a.cout = dy->c;
+  a.prologue = d->prologue;
+  a.ncit = p.ncit;
+  a.ci_chunks = p.ci_chunks;
+  a.nchunks = p.nchunks;
+  a.slab = p.slab;
+  a.want_bias = dbias != nullptr;
+  if (a.nvox > 0) {
+    const bool w2 = p.ncoiw == 2;
+    switch (p.nco) {
+#define PWW_CASE(N)                                                                   \
+  case N:                                                                             \
+    if (w2) launch_wgrad_pw<N, 2>(a, p.nsplit, s); else launch_wgrad_pw<N, 1>(a, p.nsplit, s); \
+    break;
+      PWW_CASE(2) PWW_CASE(3) PWW_CASE(4) PWW_CASE(5) PWW_CASE(6) PWW_CASE(7) PWW_CASE(8)
+#undef PWW_CASE
+      default:
+        return 0;
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      vsrk_set_error("conv_wgrad_pw: launch failed: %s", hipGetErrorString(e));
+      return -VSRK_ERR_LAUNCH;
+    }
+  } else {
+    // no voxels: the gradient is zero (the reduce below sums nothing)
+  }
+  const int64_t total = (int64_t)dy->c * x->c + (dbias ? dy->c : 0);
+  pw_wgrad_reduce<<<(int)ceil_div64(total, 256), 256, 0, s>>>(
+      (const float*)workspace, dw, dbias, a.nvox > 0 ? p.nsplit : 0, p.nchunks, p.slab, dy->c, x->c, 32 * p.nco,
+      32 * p.ncit, p.ci_chunks, dy_scale, accumulate);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    vsrk_set_error("conv_wgrad_pw_reduce: launch failed: %s", hipGetErrorString(e));
+    return -VSRK_ERR_LAUNCH;
+  }
+  return 1;
+}

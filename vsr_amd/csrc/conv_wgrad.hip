@@ -377,7 +377,7 @@ static WgradPlan wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, cons
 
 extern "C" size_t vsrk_conv_wgrad_workspace_size(const vsrk_conv_desc* d, const vsrk_tensor5* x,
                                                  const vsrk_tensor5* dy) {
-  return wgrad_plan(d, x, dy).ws_bytes;
+  return std::max(wgrad_plan(d, x, dy).ws_bytes, vsrk_conv_wgrad_pw_workspace(d, x, dy));
 }
 
 template <typename T, int NCO, int NCI, int KK, bool VEC>
@@ -412,6 +412,10 @@ extern "C" int vsrk_conv_wgrad(const vsrk_conv_desc* d, const vsrk_tensor5* x, c
   if (!view_ok(x, "conv_wgrad x") || !view_ok(dy, "conv_wgrad dy")) return VSRK_ERR_INVALID;
   VSRK_CHECK(d->kh == d->kw && (d->kh == 1 || d->kh == 3), "conv_wgrad: kh = kw in {1, 3}");
   VSRK_CHECK(!(d->prologue & VSRK_PRO_AFFINE) || (pro_scale && pro_shift), "conv_wgrad: affine prologue needs scale/shift");
+  hipStream_t s = (hipStream_t)stream;
+  const int pw = vsrk_conv_wgrad_pw(d, x, dy, pro_scale, pro_shift, dy_scale, perm_r, dw, dbias, accumulate,
+                                    workspace, workspace_bytes, s);
+  if (pw != 0) return pw > 0 ? VSRK_OK : -pw;
   const WgradPlan p = wgrad_plan(d, x, dy);
   VSRK_CHECK(workspace && workspace_bytes >= p.ws_bytes, "conv_wgrad: workspace %zu < %zu bytes", workspace_bytes,
              p.ws_bytes);
@@ -443,7 +447,6 @@ extern "C" int vsrk_conv_wgrad(const vsrk_conv_desc* d, const vsrk_tensor5* x, c
   a.cin_pad = round_up(x->c, 32 * p.nci);
   if (p.ntiles == 0) return VSRK_OK;
   const bool vec = a.xvec && a.dyvec;
-  hipStream_t s = (hipStream_t)stream;
   if (x->dtype == VSRK_BF16 && vsrk_conv_wgrad_thin(a, p.nco, p.nci, perm_r, s)) {
     // thin-channel kernel (conv_thin.hip), same slab layout
   } else if (x->dtype == VSRK_BF16 && vec && vsrk_conv_wgrad_fast(a, p.nco, p.nci, s)) {

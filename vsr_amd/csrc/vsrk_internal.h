@@ -26,7 +26,18 @@ int vsrk_conv_fwd_k3(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
                      const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                      const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
 
+// pointwise (1x1x1) bf16 conv (conv_pw.hip): forward / data gradient and
+// weight gradient; same return convention (the wgrad launches its own reduce)
+int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                     const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
+                     const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
+size_t vsrk_conv_wgrad_pw_workspace(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk_tensor5* dy);
+int vsrk_conv_wgrad_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk_tensor5* dy,
+                       const float* pro_scale, const float* pro_shift, float dy_scale, int32_t perm_r, float* dw,
+                       float* dbias, int32_t accumulate, void* workspace, size_t workspace_bytes, hipStream_t s);
+
 // path switches (vsrk_conv_set_path): -1 = from the environment, 0 off, 1 on
+extern int vsrk_g_pw_mode;
 extern int vsrk_g_k3_mode;
 extern int vsrk_g_thin_mode;
 extern int vsrk_g_wgrad_fast_mode;
