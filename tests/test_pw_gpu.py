@@ -36,13 +36,14 @@ def grid_cap(request):
     F.set_grid_cap(0)
 
 
+@pytest.mark.parametrize("dhw", [(3, 7, 19), (2, 8, 32)])
 @pytest.mark.parametrize("c", [64, 80, 96, 128, 160, 192, 224, 256])
-def test_pw_forward_prologue_slices(c, grid_cap):
+def test_pw_forward_prologue_slices(c, dhw, grid_cap):
     """BN-affine+ReLU prologue on a channel slice of a concat buffer, output into
     a channel slice of another buffer, bias; tails of voxels (N*D*H*W not a
-    multiple of the tile)."""
+    multiple of the tile) and tiles aligned to samples (d*h*w % 128 == 0)."""
     g = torch.Generator().manual_seed(c)
-    n, d, h, w = 2, 3, 7, 19
+    n, (d, h, w) = 2, dhw
     big = torch.randn((n, d, h, w, c + 40), generator=g)
     wt = torch.randn((c, c), generator=g) / c ** 0.5
     b = torch.randn(c, generator=g)

@@ -54,12 +54,56 @@ static int pw_num_cus() {
   return n;
 }
 
-// Voxel v of a view whose (d, h, w) block is dense (sd = h*sh, sh = w*sw):
-// element offset n*sn + r*sw with n = v / dhw, r = v % dhw.
-__device__ __forceinline__ int64_t vox_off(int64_t v, int dhw, int64_t sn, int64_t sw) {
-  const int n = (int)(v / dhw);
-  const int r = (int)(v - (int64_t)n * dhw);
-  return n * sn + (int64_t)r * sw;
+// Division by a launch constant d (dividends < 2^31), branch-free:
+// q = (x * mul) >> p with p = 31 + ceil(log2 d), mul = ceil(2^p / d) < 2^32.
+struct FastDiv {
+  uint32_t d, mul, p;
+};
+static FastDiv make_fastdiv(int d) {
+  int l = 0;
+  while ((1u << l) < (uint32_t)d) ++l;
+  const uint32_t p = 31 + l;
+  return FastDiv{(uint32_t)d, (uint32_t)(((1ull << p) + (uint64_t)d - 1) / (uint64_t)d), p};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
+  return (uint32_t)(((uint64_t)x * f.mul) >> f.p);
+}
+
+// Raw buffer resource over [base, base + 2 GiB) (wave-uniform base): offsets
+// at or beyond 0x7FFFFFF0 read as zero and drop stores -- the out-of-range
+// voxels and channels of a tile, without branches.
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+constexpr uint32_t PW_OOB = 0x80000000u;
+__device__ __forceinline__ Rsrc rsrc_at(const void* base) {
+  const uint64_t b = (uint64_t)base;
+  const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)u, 0, 0x7FFFFFF0, 0x00020000);
+}
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+// LDS access by 32-bit byte address (plain vector types: HIP's uint4 class has
+// no address-space-qualified copy)
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 lds_ld16(uint32_t addr) {
+  return __builtin_bit_cast(uint4, *(const __attribute__((address_space(3))) u32x4_t*)(size_t)addr);
+}
+__device__ __forceinline__ float4 lds_ldf4(uint32_t addr) {
+  return __builtin_bit_cast(float4, *(const __attribute__((address_space(3))) f32x4_t*)(size_t)addr);
+}
+__device__ __forceinline__ void lds_st8(uint32_t addr, uint2 v) {
+  *(__attribute__((address_space(3))) u32x2_t*)(size_t)addr = __builtin_bit_cast(u32x2_t, v);
+}
+typedef int v2i_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 bload16(Rsrc r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ uint2 bload8(Rsrc r, uint32_t off) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void bstore8(Rsrc r, uint32_t off, uint2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, v), r, (int)off, 0, 0);
 }
 
 __device__ __forceinline__ uint4 bf16x8_affine(uint4 v, const float4& s0, const float4& s1, const float4& h0,
@@ -85,14 +129,34 @@ struct PwArgs {
   const float* pro_scale;
   const float* pro_shift;
   const float* mask_slope;
-  int64_t xsn, xsw, ysn, ysw, msn, msw;
-  int64_t nvox;
-  int dhw;
+  int64_t xsn, xsw, ysn, ysw, msn, msw;  // element strides
+  int nvox, dhw;
+  FastDiv fd;                             // division by dhw
   int cin, cout, ci_pad, co_rows;
   int prologue, act, accumulate, has_mask;
   float out_scale;
   int ntiles;  // tiles of 32*M voxels
+  int ablate;  // A/B knob (VSRK_PW_ABLATE): 1 = no stores, 2 = no MFMA, 4 = no loads (staged)
 };
+
+// Byte offsets of a tile's voxels relative to the sample that holds its first
+// voxel: lane voxel v = v0 + k (k < 32*M) -> (n - n0) * sn + r * sw.
+struct TileBase {
+  int n0, r0;
+};
+__device__ __forceinline__ TileBase tile_base(int v0, const FastDiv& fd) {
+  const int n0 = (int)fdiv((uint32_t)v0, fd);
+  return {n0, v0 - n0 * (int)fd.d};
+}
+__device__ __forceinline__ uint32_t lane_off(const TileBase& tb, int k, int v, int nvox, const FastDiv& fd,
+                                             int64_t sn, int64_t sw) {
+  // the host guarantees these offsets fit 31 bits: 32-bit arithmetic
+  const uint32_t rel = (uint32_t)(tb.r0 + k);
+  const uint32_t dn = fdiv(rel, fd);
+  const uint32_t r = rel - dn * fd.d;
+  const uint32_t off = 2u * (dn * (uint32_t)sn + r * (uint32_t)sw);
+  return v < nvox ? off : PW_OOB;
+}
 
 // ---------------------------------------------------------------------------
 // forward / data gradient: y[v][co] = epi(sum_ci W[co][ci] * pro(x[v][ci]))
@@ -129,43 +193,48 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
   const bool relu_in = (a.prologue & VSRK_PRO_RELU) != 0;
   const float mslope = a.mask_slope ? *a.mask_slope : 0.f;
   const int nwaves = gridDim.x * (PW_THR / 64);
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
 
+  // B operand of k-step s: 8 channels 16s + 8hf of voxel col (zero outside)
   auto load = [&](int tile, uint4 (&b)[M][KS]) __attribute__((always_inline)) {
+    const int v0 = tile * 32 * M;
+    const TileBase tb = tile_base(v0, a.fd);
+    const Rsrc r = rsrc_at(a.x + (int64_t)tb.n0 * a.xsn);
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      const int64_t v = ((int64_t)tile * M + m) * 32 + col;
-      const bool ok = v < a.nvox;
-      const bf16* p = a.x + (ok ? vox_off(v, a.dhw, a.xsn, a.xsw) : 0) + 8 * hf;
+      const uint32_t off = lane_off(tb, m * 32 + col, v0 + m * 32 + col, a.nvox, a.fd, a.xsn, a.xsw);
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const bool cok = ok && 16 * s + 8 * hf < a.cin;
-        b[m][s] = cok ? *reinterpret_cast<const uint4*>(p + 16 * s) : make_uint4(0, 0, 0, 0);
+        const int c = 16 * s + 8 * hf;
+        b[m][s] = bload16(r, c < a.cin ? off + 2 * c : PW_OOB);
       }
     }
   };
 
   uint4 bc[M][KS];
-  int t = blockIdx.x * (PW_THR / 64) + wave;
+  int t = blockIdx.x * (PW_THR / 64) + wv;
   if (t < a.ntiles) load(t, bc);
   while (t < a.ntiles) {
     const int tn = t + nwaves;
+    const int v0 = t * 32 * M;
+    const TileBase tb = tile_base(v0, a.fd);
+    const Rsrc ry = rsrc_at(a.y + (int64_t)tb.n0 * a.ysn);
     // epilogue inputs of this tile first, then the next tile's operands: the
     // epilogue's wait (vmcnt) then leaves the prefetch in flight
     uint2 ein[EIN ? M : 1][NCB][4];
-    constexpr bool need_in = EIN;  // mask and/or accumulate
     if constexpr (EIN) {
+      const Rsrc rm = a.has_mask ? rsrc_at(a.msk + (int64_t)tb.n0 * a.msn) : ry;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        const int64_t v = ((int64_t)t * M + m) * 32 + col;
-        const bool ok = v < a.nvox;
-        const bf16* src = a.has_mask ? a.msk : a.y;
-        const int64_t off = ok ? (a.has_mask ? vox_off(v, a.dhw, a.msn, a.msw) : vox_off(v, a.dhw, a.ysn, a.ysw)) : 0;
+        const uint32_t off = a.has_mask
+                                 ? lane_off(tb, m * 32 + col, v0 + m * 32 + col, a.nvox, a.fd, a.msn, a.msw)
+                                 : lane_off(tb, m * 32 + col, v0 + m * 32 + col, a.nvox, a.fd, a.ysn, a.ysw);
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int gco = co0 + cb * 32 + 8 * j + 4 * hf;
-            ein[m][cb][j] = (ok && gco < a.cout) ? *reinterpret_cast<const uint2*>(src + off + gco) : make_uint2(0, 0);
+            ein[m][cb][j] = bload8(rm, gco < a.cout ? off + 2 * gco : PW_OOB);
           }
       }
     }
@@ -179,62 +248,63 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
       for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[m][cb][i] = 0.f;
+    if (!(a.ablate & 2)) {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      if (PRO) {
-        const int c = 16 * s + 8 * hf;
-        const float4 s0 = *reinterpret_cast<const float4*>(lsc + c), s1 = *reinterpret_cast<const float4*>(lsc + c + 4);
-        const float4 h0 = *reinterpret_cast<const float4*>(lsh + c), h1 = *reinterpret_cast<const float4*>(lsh + c + 4);
+      for (int s = 0; s < KS; ++s) {
+        if (PRO) {
+          const int c = 16 * s + 8 * hf;
+          const float4 s0 = *reinterpret_cast<const float4*>(lsc + c), s1 = *reinterpret_cast<const float4*>(lsc + c + 4);
+          const float4 h0 = *reinterpret_cast<const float4*>(lsh + c), h1 = *reinterpret_cast<const float4*>(lsh + c + 4);
 #pragma unroll
-        for (int m = 0; m < M; ++m) bc[m][s] = bf16x8_affine(bc[m][s], s0, s1, h0, h1, relu_in);
+          for (int m = 0; m < M; ++m) bc[m][s] = bf16x8_affine(bc[m][s], s0, s1, h0, h1, relu_in);
+        }
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+          const uint4 af = *reinterpret_cast<const uint4*>(lw + ((s * 2 + hf) * COP + cb * 32 + col) * 16);
+#pragma unroll
+          for (int m = 0; m < M; ++m) mma<bf16>(acc[m][cb], af, bc[m][s]);
+        }
+        // keep the scheduler from hoisting every k-step's weight reads (register pressure)
+        __builtin_amdgcn_sched_barrier(0);
       }
+    } else {
 #pragma unroll
-      for (int cb = 0; cb < NCB; ++cb) {
-        const uint4 af = *reinterpret_cast<const uint4*>(lw + ((s * 2 + hf) * COP + cb * 32 + col) * 16);
-#pragma unroll
-        for (int m = 0; m < M; ++m) mma<bf16>(acc[m][cb], af, bc[m][s]);
-      }
-      // keep the scheduler from hoisting every k-step's weight reads (register pressure)
-      __builtin_amdgcn_sched_barrier(0);
+      for (int m = 0; m < M; ++m) acc[m][0][0] = __builtin_bit_cast(float, bc[m][0].x ^ bc[m][KS - 1].w);
     }
 
     // epilogue: lane holds voxel col, channels cb*32 + 8j + 4hf + (0..3)
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      const int64_t v = ((int64_t)t * M + m) * 32 + col;
-      if (v < a.nvox) {
-        bf16* yp = a.y + vox_off(v, a.dhw, a.ysn, a.ysw);
+      const uint32_t yoff = lane_off(tb, m * 32 + col, v0 + m * 32 + col, a.nvox, a.fd, a.ysn, a.ysw);
 #pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) {
+      for (int cb = 0; cb < NCB; ++cb) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int co = cb * 32 + 8 * j + 4 * hf;
-            if (co0 + co < a.cout) {
-              const float4 bb = *reinterpret_cast<const float4*>(lb + co);
-              float o[4] = {acc[m][cb][4 * j] + bb.x, acc[m][cb][4 * j + 1] + bb.y, acc[m][cb][4 * j + 2] + bb.z,
-                            acc[m][cb][4 * j + 3] + bb.w};
-              float e4[4] = {0.f, 0.f, 0.f, 0.f};
-              if constexpr (EIN) unpack_pk<bf16>(ein[m][cb][j], e4);
+        for (int j = 0; j < 4; ++j) {
+          const int co = cb * 32 + 8 * j + 4 * hf;
+          const float4 bb = *reinterpret_cast<const float4*>(lb + co);
+          float o[4] = {acc[m][cb][4 * j] + bb.x, acc[m][cb][4 * j + 1] + bb.y, acc[m][cb][4 * j + 2] + bb.z,
+                        acc[m][cb][4 * j + 3] + bb.w};
+          float e4[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (EIN) unpack_pk<bf16>(ein[m][cb][j], e4);
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                float r = act_apply(a.act, o[e] * a.out_scale, 0.f);
-                if (a.has_mask) r = mask_apply(e4[e], r, mslope);
-                o[e] = r;
-              }
-              if (a.accumulate) {
-                if (a.has_mask) {
-                  float y4[4];
-                  unpack_pk<bf16>(*reinterpret_cast<const uint2*>(yp + co0 + co), y4);
+          for (int e = 0; e < 4; ++e) {
+            float rr = act_apply(a.act, o[e] * a.out_scale, 0.f);
+            if (a.has_mask) rr = mask_apply(e4[e], rr, mslope);
+            o[e] = rr;
+          }
+          const uint32_t so = co0 + co < a.cout ? yoff + 2 * (co0 + co) : PW_OOB;
+          if (a.accumulate) {
+            if (a.has_mask) {
+              float y4[4];
+              unpack_pk<bf16>(bload8(ry, so), y4);
 #pragma unroll
-                  for (int e = 0; e < 4; ++e) o[e] += y4[e];
-                } else {
+              for (int e = 0; e < 4; ++e) o[e] += y4[e];
+            } else {
 #pragma unroll
-                  for (int e = 0; e < 4; ++e) o[e] += e4[e];
-                }
-              }
-              *reinterpret_cast<uint2*>(yp + co0 + co) = pack_pk<bf16, uint2>(o);
+              for (int e = 0; e < 4; ++e) o[e] += e4[e];
             }
           }
+          if (!(a.ablate & 1)) bstore8(ry, so, pack_pk<bf16, uint2>(o));
         }
       }
     }
@@ -243,6 +313,190 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
       for (int m = 0; m < M; ++m)
 #pragma unroll
         for (int s = 0; s < KS; ++s) bc[m][s] = bn[m][s];
+    }
+    t = tn;
+  }
+}
+
+// Staged variant (no mask / accumulate, NCB <= 7): each wave owns an LDS
+// tile buffer [32*M voxels][CIP + 8 pad] bf16.  The next tile is fetched with
+// coalesced 16-byte loads (consecutive lanes -> consecutive bytes of a voxel
+// row, then the next row) into registers while the current tile computes; the
+// B fragments are read back from LDS (row pad: conflict-free ds_read_b128).
+// The outputs take the same way back: bf16-packed accumulators to the buffer,
+// then coalesced 16-byte row stores.  Wave-private buffer: no barriers.
+// AL: every tile lies inside one sample (d*h*w % (32*M) == 0), so a voxel
+// row's offset is row * sw from the tile's base -- the common, cheap case;
+// otherwise rows are placed with a division per row.  ACT: VSRK_ACT_NONE /
+// VSRK_ACT_RELU at compile time (the epilogue is most of the VALU work).
+template <int NCB, int M, bool PRO, bool AL, int ACT>
+__global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
+  constexpr int KS = 2 * NCB;
+  constexpr int COP = 32 * NCB;
+  constexpr int CIP = 16 * KS;
+  constexpr int RS = 2 * CIP + 16;           // buffer row stride (bytes)
+  constexpr int CPR = CIP / 8;               // 16-byte chunks per row
+  constexpr int ROWS = 32 * M;
+  constexpr int NCK = ROWS * CPR / 64;       // chunks per lane per tile (= M*KS)
+  constexpr int WBYTES = KS * 2 * COP * 16;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* lw = lds;                                         // [KS][2][COP] x 16 B
+  float* lsc = reinterpret_cast<float*>(lds + WBYTES);    // [CIP]
+  float* lsh = lsc + CIP;                                 // [CIP]
+  float* lb = reinterpret_cast<float*>(lds + WBYTES + (PRO ? 2 * CIP * 4 : 0));  // [COP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hf = lane >> 5, col = lane & 31;
+  const int co0 = blockIdx.y * COP;
+  char* buf = lds + WBYTES + (PRO ? 2 * CIP * 4 : 0) + COP * 4 + wave * (ROWS * RS);
+
+  for (int i = tid; i < KS * 2 * COP; i += PW_THR) {
+    const int co = i % COP, t = i / COP, h = t & 1, s = t >> 1;
+    const int ci = 16 * s + 8 * h;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (ci < a.ci_pad && co0 + co < a.co_rows)
+      v = *reinterpret_cast<const uint4*>(a.w + (int64_t)(co0 + co) * a.ci_pad + ci);
+    *reinterpret_cast<uint4*>(lw + i * 16) = v;
+  }
+  if (PRO) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, CIP, tid, PW_THR);
+  for (int i = tid; i < COP; i += PW_THR) lb[i] = (a.bias && co0 + i < a.cout) ? a.bias[co0 + i] : 0.f;
+  __syncthreads();
+
+  const bool relu_in = (a.prologue & VSRK_PRO_RELU) != 0;
+  const int nwaves = gridDim.x * (PW_THR / 64);
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const float osc = a.out_scale;
+
+  // byte offset of tile row `row` (voxel v0 + row) from the tile's sample base
+  auto row_off = [&](const TileBase& tb, int row, int v0, int64_t sn, int64_t sw) __attribute__((always_inline)) {
+    if constexpr (AL) {
+      return (uint32_t)(2 * (tb.r0 + row) * (uint32_t)sw);
+    } else {
+      return lane_off(tb, row, v0 + row, a.nvox, a.fd, sn, sw);
+    }
+  };
+
+  // fixed chunk roles: chunk k of a lane = row (lane + 64k) / CPR, column % CPR.
+  // `ln` = lane through an opaque copy per use site: the per-chunk offsets
+  // derived from it are recomputed (a few VALU) instead of held in VGPRs.
+  auto load = [&](int tile, uint4 (&r)[NCK]) __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int v0 = tile * ROWS;
+    const TileBase tb = tile_base(v0, a.fd);
+    const Rsrc rs = rsrc_at(a.x + (int64_t)tb.n0 * a.xsn);
+#pragma unroll
+    for (int k = 0; k < NCK; ++k) {
+      const int i = ln + 64 * k, row = i / CPR, c = 8 * (i % CPR);
+      const uint32_t off = row_off(tb, row, v0, a.xsn, a.xsw);
+      r[k] = bload16(rs, c < a.cin ? off + 2 * c : PW_OOB);
+    }
+  };
+  auto put = [&](const uint4 (&r)[NCK]) __attribute__((always_inline)) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int k = 0; k < NCK; ++k) {
+      const int i = ln + 64 * k, row = i / CPR, c = i % CPR;
+      *reinterpret_cast<uint4*>(buf + row * RS + c * 16) = r[k];
+    }
+  };
+
+  uint4 rg[NCK];
+  int t = blockIdx.x * (PW_THR / 64) + wv;
+  if (t < a.ntiles) load(t, rg);
+  while (t < a.ntiles) {
+    const int tn = t + nwaves;
+    put(rg);
+    if (tn < a.ntiles) load(tn, rg);  // in flight during this tile's MFMAs and stores
+
+    f32x16 acc[M][NCB];
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[m][cb][i] = 0.f;
+    // k-step s+1's fragments (and prologue constants) are read while step s's MFMAs run
+    struct Frag {
+      uint4 a[NCB], b[M];
+      float4 s0, s1, h0, h1;
+    };
+    // LDS byte addresses from opaque per-tile bases: the compiler would otherwise
+    // hoist one VGPR per (k-step, block) address out of the tile loop (offsets
+    // past the 64 KiB immediate range) and starve the fragment pipeline
+    uint32_t abase = lds_addr(lw) + (hf * COP + col) * 16;
+    uint32_t bbase = lds_addr(buf) + col * RS + hf * 16;
+    asm volatile("" : "+v"(abase), "+v"(bbase));
+    auto rd = [&](int s, Frag& f) __attribute__((always_inline)) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) f.b[m] = lds_ld16(bbase + m * 32 * RS + 32 * s);
+      const uint32_t as = abase + s * 2 * COP * 16;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) f.a[cb] = lds_ld16(as + cb * 32 * 16);
+      if (PRO) {
+        const int c = 16 * s + 8 * hf;
+        f.s0 = *reinterpret_cast<const float4*>(lsc + c);
+        f.s1 = *reinterpret_cast<const float4*>(lsc + c + 4);
+        f.h0 = *reinterpret_cast<const float4*>(lsh + c);
+        f.h1 = *reinterpret_cast<const float4*>(lsh + c + 4);
+      }
+    };
+    Frag fr[2];
+    rd(0, fr[0]);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      Frag& f = fr[s & 1];
+      if (s + 1 < KS) rd(s + 1, fr[(s + 1) & 1]);
+      if (PRO) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) f.b[m] = bf16x8_affine(f.b[m], f.s0, f.s1, f.h0, f.h1, relu_in);
+      }
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int m = 0; m < M; ++m) mma<bf16>(acc[m][cb], f.a[cb], f.b[m]);
+    }
+
+    // epilogue into the buffer (row = voxel, COP bf16 channels), then row stores
+    {
+      uint32_t ebase = lds_addr(buf) + col * RS + hf * 8;
+      uint32_t bias_b = lds_addr(lb) + hf * 16;
+      asm volatile("" : "+v"(ebase), "+v"(bias_b));
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 bb = lds_ldf4(bias_b + (cb * 32 + 8 * j) * 4);
+#pragma unroll
+          for (int m = 0; m < M; ++m) {
+            float o[4] = {acc[m][cb][4 * j] + bb.x, acc[m][cb][4 * j + 1] + bb.y, acc[m][cb][4 * j + 2] + bb.z,
+                          acc[m][cb][4 * j + 3] + bb.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              o[e] *= osc;
+              if constexpr (ACT == VSRK_ACT_RELU) o[e] = fmaxf(o[e], 0.f);
+            }
+            lds_st8(ebase + m * 32 * RS + (cb * 32 + 8 * j) * 2, pack_pk<bf16, uint2>(o));
+          }
+        }
+    }
+    {
+      const int v0 = t * ROWS;
+      const TileBase tb = tile_base(v0, a.fd);
+      const Rsrc ry = rsrc_at(a.y + (int64_t)tb.n0 * a.ysn);
+      constexpr int OCPR = COP / 8;
+      constexpr int NOK = ROWS * OCPR / 64;
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+#pragma unroll
+      for (int k = 0; k < NOK; ++k) {
+        const int i = ln + 64 * k, row = i / OCPR, c = 8 * (i % OCPR);
+        const uint4 v = *reinterpret_cast<const uint4*>(buf + row * RS + c * 2);
+        const uint32_t off = row_off(tb, row, v0, a.ysn, a.ysw);
+        if (!(a.ablate & 1))
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), ry,
+                                                 (int)(co0 + c < a.cout ? off + 2 * (co0 + c) : PW_OOB), 0, 0);
+      }
     }
     t = tn;
   }
@@ -257,9 +511,9 @@ struct PwWArgs {
   const float* pro_scale;
   const float* pro_shift;
   float* ws;
-  int64_t xsn, xsw, dsn, dsw;
-  int64_t nvox, vox_per_split;
-  int dhw;
+  int64_t xsn, xsw, dsn, dsw;  // element strides
+  int nvox, vox_per_split, dhw;
+  FastDiv fd;
   int cin, cout, prologue;
   int ncit;                  // ci blocks in this launch's chunks (<= 4*NCIW)
   int ci_chunks, nchunks;    // blockIdx.y = co_chunk * ci_chunks + ci_chunk
@@ -270,60 +524,74 @@ struct PwWArgs {
 // NCO dY channel blocks per chunk; wave w owns X blocks w, w+4 (NCIW of them).
 template <int NCO, int NCIW>
 __global__ __launch_bounds__(PW_THR, 1) void pw_wgrad_kernel(PwWArgs a) {
-  constexpr int PLMAX = NCO + 4 * NCIW;  // 32-channel planes per stage (max)
-  constexpr int PSZ = PW_KP * 64;        // bytes per plane: 64 voxel rows of 32 bf16
+  constexpr int NCIMAX = 4 * NCIW;
+  constexpr int PLMAX = NCO + NCIMAX;   // 32-channel planes per stage (max)
+  constexpr int PSZ = PW_KP * 64;       // bytes per plane: 64 voxel rows of 32 bf16
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int PL = NCO + a.ncit;
-  const int NCH = PL * 4;            // 16-byte chunks per voxel
   const int split = blockIdx.x, chunk = blockIdx.y;
   const int co_chunk = chunk / a.ci_chunks, ci_chunk = chunk - co_chunk * a.ci_chunks;
   const int co0 = co_chunk * 32 * NCO, ci0 = ci_chunk * 32 * a.ncit;
-  const int64_t vbeg = (int64_t)split * a.vox_per_split;
-  const int64_t vend = std::min<int64_t>(a.nvox, vbeg + a.vox_per_split);
-  const int nst = vend > vbeg ? (int)((vend - vbeg + PW_KP - 1) / PW_KP) : 0;
+  const int vbeg = split * a.vox_per_split;
+  const int vend = min(a.nvox, vbeg + a.vox_per_split);
+  const int nst = vend > vbeg ? (vend - vbeg + PW_KP - 1) / PW_KP : 0;
   const bool relu_in = (a.prologue & VSRK_PRO_RELU) != 0;
   const bool aff = (a.prologue & VSRK_PRO_AFFINE) != 0;
   const bool do_bias = a.want_bias && ci_chunk == 0 && wave == 0;
 
-  // per-thread chunk roles (PL chunks per thread per stage)
-  uint4 rg[PLMAX];
-  auto issue = [&](int st) __attribute__((always_inline)) {
-    const int64_t v0 = vbeg + (int64_t)st * PW_KP;
-    const int n0 = (int)(v0 / a.dhw);
-    const int r0 = (int)(v0 - (int64_t)n0 * a.dhw);
+  // Per-thread chunk roles, fixed for the whole loop: dY chunk k (< NCO) and X
+  // chunk k (< ncit) are 16-byte pieces i = tid + 256k of the stage's
+  // [voxel][plane][4 x 16 B] image; every load instruction reads one tensor.
+  int dvox[NCO], dch[NCO], dlds[NCO];
 #pragma unroll
-    for (int k = 0; k < PLMAX; ++k) {
-      if (k < PL) {
-        const int i = tid + k * PW_THR;
-        const int vox = i / NCH, within = i - vox * NCH;
-        const int plane = within >> 2, q = within & 3;
-        int n = n0, r = r0 + vox;
-        while (r >= a.dhw) { r -= a.dhw; ++n; }
-        const bool vok = v0 + vox < vend;
-        uint4 val = make_uint4(0, 0, 0, 0);
-        if (plane < NCO) {
-          const int c = co0 + plane * 32 + q * 8;
-          if (vok && c < a.cout) val = *reinterpret_cast<const uint4*>(a.dy + n * a.dsn + (int64_t)r * a.dsw + c);
-        } else {
-          const int c = ci0 + (plane - NCO) * 32 + q * 8;
-          if (vok && c < a.cin) val = *reinterpret_cast<const uint4*>(a.x + n * a.xsn + (int64_t)r * a.xsw + c);
-        }
-        rg[k] = val;
+  for (int k = 0; k < NCO; ++k) {
+    const int i = tid + k * PW_THR;
+    const int vox = i / (4 * NCO), within = i - vox * (4 * NCO);
+    const int plane = within >> 2, q = within & 3;
+    dvox[k] = vox;
+    const int c = co0 + plane * 32 + q * 8;
+    dch[k] = c < a.cout ? 2 * c : -1;
+    dlds[k] = plane * PSZ + vox * 64 + q * 16;
+  }
+  int xvox[NCIMAX], xch[NCIMAX], xlds[NCIMAX];
+  const int nxc = 4 * a.ncit;
+#pragma unroll
+  for (int k = 0; k < NCIMAX; ++k) {
+    const int i = tid + k * PW_THR;
+    const int vox = i / nxc, within = i - vox * nxc;
+    const int plane = within >> 2, q = within & 3;
+    xvox[k] = vox;
+    const int c = ci0 + plane * 32 + q * 8;
+    xch[k] = (k < a.ncit && c < a.cin) ? 2 * c : -1;
+    xlds[k] = (NCO + plane) * PSZ + vox * 64 + q * 16;
+  }
+
+  uint4 ry[NCO], rx[NCIMAX];
+  auto issue = [&](int st) __attribute__((always_inline)) {
+    const int v0 = vbeg + st * PW_KP;
+    const TileBase tb = tile_base(v0, a.fd);
+    const Rsrc rdy = rsrc_at(a.dy + (int64_t)tb.n0 * a.dsn);
+    const Rsrc rxx = rsrc_at(a.x + (int64_t)tb.n0 * a.xsn);
+#pragma unroll
+    for (int k = 0; k < NCO; ++k) {
+      const uint32_t off = lane_off(tb, dvox[k], v0 + dvox[k], vend, a.fd, a.dsn, a.dsw);
+      ry[k] = bload16(rdy, dch[k] >= 0 ? off + dch[k] : PW_OOB);
+    }
+#pragma unroll
+    for (int k = 0; k < NCIMAX; ++k) {
+      if (k < a.ncit) {
+        const uint32_t off = lane_off(tb, xvox[k], v0 + xvox[k], vend, a.fd, a.xsn, a.xsw);
+        rx[k] = bload16(rxx, xch[k] >= 0 ? off + xch[k] : PW_OOB);
       }
     }
   };
   auto commit = [&](int buf) __attribute__((always_inline)) {
     char* base = lds + buf * (PLMAX * PSZ);
 #pragma unroll
-    for (int k = 0; k < PLMAX; ++k) {
-      if (k < PL) {
-        const int i = tid + k * PW_THR;
-        const int vox = i / NCH, within = i - vox * NCH;
-        const int plane = within >> 2, q = within & 3;
-        *reinterpret_cast<uint4*>(base + plane * PSZ + vox * 64 + q * 16) = rg[k];
-      }
-    }
+    for (int k = 0; k < NCO; ++k) *reinterpret_cast<uint4*>(base + dlds[k]) = ry[k];
+#pragma unroll
+    for (int k = 0; k < NCIMAX; ++k)
+      if (k < a.ncit) *reinterpret_cast<uint4*>(base + xlds[k]) = rx[k];
   };
 
   // prologue scale/shift of the lane's X channel in each owned block
@@ -433,36 +701,55 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_wgrad_kernel(PwWArgs a) {
 }
 
 // dw[co][ci] (torch layout of a 1x1x1 weight, fp32) [+]= scale * sum over
-// splits of the slabs, in split order; then dbias.
+// splits of the slabs; then dbias.  A block = 32 consecutive outputs x 8 split
+// groups; group g sums splits g, g+8, ... in order (4 loads in flight), the 8
+// partials are added in a fixed order: deterministic.
 __global__ __launch_bounds__(256) void pw_wgrad_reduce(const float* __restrict__ ws, float* __restrict__ dw,
                                                       float* __restrict__ db, int nsplit, int nchunks, int slab,
                                                       int cout, int cin, int cop, int cic, int ci_chunks,
                                                       float scale, int accumulate) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float part[8][32];
+  const int l = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int64_t idx = (int64_t)blockIdx.x * 32 + l;
   const int64_t nw = (int64_t)cout * cin;
-  if (idx >= nw + (db ? cout : 0)) return;
-  int co, ci;
-  const float* p;
-  const int64_t sstride = (int64_t)nchunks * slab;
+  const int64_t total = nw + (db ? cout : 0);
+  const float* p = nullptr;
+  int co = 0;
   if (idx < nw) {
     co = (int)(idx / cin);
-    ci = (int)(idx - (int64_t)co * cin);
+    const int ci = (int)(idx - (int64_t)co * cin);
     const int chunk = (co / cop) * ci_chunks + ci / cic;
     p = ws + (int64_t)chunk * slab + (int64_t)(co % cop) * cic + (ci % cic);
-  } else {
+  } else if (idx < total) {
     co = (int)(idx - nw);
-    ci = 0;
     const int chunk = (co / cop) * ci_chunks;
     p = ws + (int64_t)chunk * slab + (int64_t)cop * cic + (co % cop);
   }
   float s = 0.f;
-  for (int k = 0; k < nsplit; ++k) s += p[k * sstride];
-  s *= scale;
+  if (p) {
+    const int64_t ss = (int64_t)nchunks * slab;
+    int k = grp;
+    for (; k + 24 < nsplit; k += 32) {
+      const float a0 = p[k * ss], a1 = p[(k + 8) * ss], a2 = p[(k + 16) * ss], a3 = p[(k + 24) * ss];
+      s += a0;
+      s += a1;
+      s += a2;
+      s += a3;
+    }
+    for (; k < nsplit; k += 8) s += p[k * ss];
+  }
+  part[grp][l] = s;
+  __syncthreads();
+  if (grp != 0 || idx >= total) return;
+  float t = part[0][l];
+#pragma unroll
+  for (int g = 1; g < 8; ++g) t += part[g][l];
+  t *= scale;
   if (idx < nw) {
     float* d = dw + idx;
-    *d = accumulate ? *d + s : s;
+    *d = accumulate ? *d + t : t;
   } else {
-    db[co] = accumulate ? db[co] + s : s;
+    db[co] = accumulate ? db[co] + t : t;
   }
 }
 
@@ -477,12 +764,36 @@ static bool dhw_dense(const vsrk_tensor5* t) {
 template <int NCB, int M>
 static void launch_fwd(const PwArgs& a, int nchunk, bool pro, hipStream_t s) {
   constexpr int KS = 2 * NCB, COP = 32 * NCB, CIP = 16 * KS;
-  const size_t lds = (size_t)KS * 2 * COP * 16 + (2 * CIP + COP) * sizeof(float);
-  const int64_t waves = (a.ntiles + 0);
-  int grid = (int)std::min<int64_t>(pw_num_cus(), ceil_div64(waves, PW_THR / 64));
+  int grid = (int)std::min<int64_t>(pw_num_cus(), ceil_div64(a.ntiles, PW_THR / 64));
   if (vsrk_g_grid_cap > 0) grid = std::min(grid, vsrk_g_grid_cap);
   grid = std::max(grid, 1);
   const bool ein = a.has_mask || a.accumulate;
+  if constexpr (NCB <= 7) {
+    static int staged = -1;
+    if (staged < 0) {
+      const char* e = getenv("VSRK_PW_STAGED");
+      staged = (e && e[0] == '0') ? 0 : 1;
+    }
+    if (!ein && staged && a.cout % 8 == 0) {
+      const size_t lds =
+          (size_t)KS * 2 * COP * 16 + (pro ? 2 * CIP * 4 : 0) + COP * 4 + 4 * (32 * M) * (2 * CIP + 16);
+      const bool al = a.dhw % (32 * M) == 0;
+      const bool relu = a.act == VSRK_ACT_RELU;
+      using K = void (*)(PwArgs);
+      K kern;
+      if (pro) {
+        if (al) kern = relu ? pw_fwd_staged_kernel<NCB, M, true, true, 1> : pw_fwd_staged_kernel<NCB, M, true, true, 0>;
+        else kern = relu ? pw_fwd_staged_kernel<NCB, M, true, false, 1> : pw_fwd_staged_kernel<NCB, M, true, false, 0>;
+      } else {
+        if (al) kern = relu ? pw_fwd_staged_kernel<NCB, M, false, true, 1> : pw_fwd_staged_kernel<NCB, M, false, true, 0>;
+        else kern = relu ? pw_fwd_staged_kernel<NCB, M, false, false, 1> : pw_fwd_staged_kernel<NCB, M, false, false, 0>;
+      }
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      kern<<<dim3(grid, nchunk), PW_THR, lds, s>>>(a);
+      return;
+    }
+  }
+  const size_t lds = (size_t)KS * 2 * COP * 16 + (2 * CIP + COP) * sizeof(float);
   auto kern = pro ? (ein ? pw_fwd_kernel<NCB, M, true, true> : pw_fwd_kernel<NCB, M, true, false>)
                   : (ein ? pw_fwd_kernel<NCB, M, false, true> : pw_fwd_kernel<NCB, M, false, false>);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -529,7 +840,23 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
   a.msn = mask ? mask->sn : 0;
   a.msw = mask ? mask->sw : 0;
   a.dhw = x->d * x->h * x->w;
-  a.nvox = (int64_t)x->n * a.dhw;
+  const int64_t nvox = (int64_t)x->n * a.dhw;
+  if (nvox >= (1ll << 31) - 4096) return 0;
+  a.nvox = (int)nvox;
+  a.fd = make_fastdiv(std::max(a.dhw, 1));
+  {
+    // lane offsets relative to a tile's first sample stay below 2 GiB
+    const int64_t span_n = 32 * 4 / std::max(a.dhw, 1) + 2;
+    for (const vsrk_tensor5* t : {x, y, mask}) {
+      if (t && 2 * (span_n * t->sn + (int64_t)a.dhw * t->sw + t->c) >= 0x7FFFFFF0ll) return 0;
+    }
+  }
+  static int ablate = -1;
+  if (ablate < 0) {
+    const char* e = getenv("VSRK_PW_ABLATE");
+    ablate = e ? atoi(e) : 0;
+  }
+  a.ablate = ablate;
   a.cin = x->c;
   a.cout = y->c;
   a.ci_pad = cip;
@@ -544,7 +871,7 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
   switch (ncb) {
 #define PW_CASE(N)                                                     \
   case N:                                                              \
-    a.ntiles = (int)ceil_div64(a.nvox, 32 * pw_m<N>());                \
+    a.ntiles = ceil_div(a.nvox, 32 * pw_m<N>());                       \
     launch_fwd<N, pw_m<N>()>(a, nchunk, pro, s);                       \
     break;
     PW_CASE(2) PW_CASE(3) PW_CASE(4) PW_CASE(5) PW_CASE(6) PW_CASE(7) PW_CASE(8)
@@ -586,8 +913,17 @@ PwWPlan pw_wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk
   p.ncoiw = ceil_div(p.ncit, 4);
   p.nchunks = p.co_chunks * p.ci_chunks;
   const int64_t nvox = (int64_t)x->n * x->d * x->h * x->w;
+  if (nvox >= (1ll << 31) - 4096) return p;
+  {
+    const int dhw = std::max(x->d * x->h * x->w, 1);
+    const int64_t span_n = PW_KP / dhw + 2;
+    for (const vsrk_tensor5* t : {x, dy})
+      if (2 * (span_n * t->sn + (int64_t)dhw * t->sw + t->c) >= 0x7FFFFFF0ll) return p;
+  }
   const int64_t steps = std::max<int64_t>(1, ceil_div64(nvox, PW_KP));
-  int want = std::max(1, pw_num_cus() / p.nchunks);
+  // two workgroups per CU where the double-buffered stage fits LDS twice
+  const size_t lds = (size_t)2 * (p.nco + 4 * p.ncoiw) * PW_KP * 64;
+  int want = std::max(1, pw_num_cus() * (lds <= 80 * 1024 ? 2 : 1) / p.nchunks);
   if (vsrk_g_grid_cap > 0) want = std::max(1, vsrk_g_grid_cap / p.nchunks);
   want = (int)std::min<int64_t>(want, steps);
   p.vps = ceil_div64(steps, want) * PW_KP;
@@ -631,9 +967,10 @@ int vsrk_conv_wgrad_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsr
   a.ws = (float*)workspace;
   a.xsn = x->sn; a.xsw = x->sw;
   a.dsn = dy->sn; a.dsw = dy->sw;
-  a.nvox = (int64_t)x->n * x->d * x->h * x->w;
-  a.vox_per_split = p.vps;
+  a.nvox = x->n * x->d * x->h * x->w;
+  a.vox_per_split = (int)p.vps;
   a.dhw = x->d * x->h * x->w;
+  a.fd = make_fastdiv(std::max(a.dhw, 1));
   a.cin = x->c;
   a.cout = dy->c;
   a.prologue = d->prologue;
@@ -663,7 +1000,7 @@ int vsrk_conv_wgrad_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsr
     // no voxels: the gradient is zero (the reduce below sums nothing)
   }
   const int64_t total = (int64_t)dy->c * x->c + (dbias ? dy->c : 0);
-  pw_wgrad_reduce<<<(int)ceil_div64(total, 256), 256, 0, s>>>(
+  pw_wgrad_reduce<<<(int)ceil_div64(total, 32), 256, 0, s>>>(
       (const float*)workspace, dw, dbias, a.nvox > 0 ? p.nsplit : 0, p.nchunks, p.slab, dy->c, x->c, 32 * p.nco,
       32 * p.ncit, p.ci_chunks, dy_scale, accumulate);
   hipError_t e = hipGetLastError();
