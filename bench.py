@@ -82,7 +82,7 @@ def _vox(v) -> int:
     return v.n * v.d * v.h * v.w
 
 
-def dominant(model):
+def dominant(model, precision="bf16"):
     """(matcher, description).  matcher(kind, xv, yv) -> algorithmic FLOP of the
     launch (counted as the forward conv's 2*cin*cout*taps per forward output
     voxel) when it is one of the roofline kernels, else 0.  xv/yv are the
@@ -95,7 +95,7 @@ def dominant(model):
                 return 0
             return 2 * 64 * 64 * 9 * _vox(yv)  # fwd: y is the output; dgrad: same size; wgrad: yv = dy
 
-        return match, (f"EDSR body conv3x3 64->64 bf16 implicit-GEMM, fwd + dgrad + wgrad per layer, "
+        return match, (f"EDSR body conv3x3 64->64 {precision} implicit-GEMM, fwd + dgrad + wgrad per layer, "
                        f"{B * T}x{H}x{W} per launch (33 layers)")
     if model == "duf":
         def match(kind, xv, yv):
@@ -109,7 +109,7 @@ def dominant(model):
                 return 2 * 27 * yv.c * 32 * _vox(xv)
             return 0
 
-        return match, (f"DUF Conv3d 3x3x3 F->32 (F = 64..224) bf16 implicit-GEMM, fwd + dgrad + wgrad, "
+        return match, (f"DUF Conv3d 3x3x3 F->32 (F = 64..224) {precision} implicit-GEMM, fwd + dgrad + wgrad, "
                        f"{B * T} windows x 7 x {H}x{W}")
 
     def match(kind, xv, yv):
@@ -224,7 +224,7 @@ def run_model(name, args, world, rank, dev):
 
     for _ in range(args.warmup):
         step()
-    match, kdesc = dominant(name)
+    match, kdesc = dominant(name, args.precision)
     F.timer = F.KernelTimer(match)
     if world > 1:
         dist.barrier()
@@ -321,7 +321,7 @@ def main():
     ap.add_argument("--models", default=os.environ.get("VSR_BENCH_MODELS", "edsr,duf"),
                     help="comma-separated subset of " + ",".join(MODELS))
     ap.add_argument("--model", default=None, help="a single model (same as --models NAME)")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     if args.model:

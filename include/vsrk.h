@@ -37,7 +37,10 @@ enum {
   VSRK_ERR_LAUNCH = 3        /* HIP launch failure */
 };
 
-enum { VSRK_F32 = 0, VSRK_BF16 = 1 };
+/* Element types of vsrk_tensor5 views and packed weights.  Every kernel
+ * family computes in fp32 accumulators; 16-bit inputs use the MFMA of their
+ * type (bf16 or fp16). */
+enum { VSRK_F32 = 0, VSRK_BF16 = 1, VSRK_F16 = 2 };
 
 enum { VSRK_PRO_NONE = 0, VSRK_PRO_RELU = 1, VSRK_PRO_AFFINE = 2, VSRK_PRO_AFFINE_RELU = 3 };
 enum { VSRK_ACT_NONE = 0, VSRK_ACT_RELU = 1, VSRK_ACT_PRELU = 2 };

@@ -22,6 +22,9 @@ fp32 HIP path: output max |d| <= max(1e-4, 3*out_err32); gradient rel-L2 <=
   checked at 1e-5..1e-4 against fp64 in test_bn_duf_kernels_gpu.py.
   Parameters whose exact gradient is 0 (conv biases feeding a BatchNorm):
   |g| <= 1e-4 * max gradient norm.
+fp16 HIP path (loss-scaled backward, BaseNet._loss_scale): the bf16 bounds
+  scaled by the 8x finer rounding: output max |d| <= 5e-3, mean <= 5e-4,
+  gradient rel-L2 <= max(1e-2, bf16_env / 4, 3 * ref32_err).
 bf16 HIP path: output max |d| <= 3e-2, mean |d| <= 3e-3; gradient rel-L2 <=
   max(8e-2, 2*bf16_env) where bf16_env is the error of an *ideal*
   bf16-storage implementation (fp64 math, bf16 weights, every conv/BN output
@@ -118,7 +121,7 @@ def _rel(g, fx, k, full_key="grad_full64", proj_key="grad_proj64", norm_key="gra
     return e.pow(2).mean().sqrt().item() / fx[norm_key][k]
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp16"])
 @pytest.mark.parametrize("name", CASES)
 def test_net_matches_golden(name, precision):
     fx = load_golden(name)
@@ -132,24 +135,30 @@ def test_net_matches_golden(name, precision):
     d = (got - exp).abs()
     if precision == "fp32":
         assert d.max().item() <= max(1e-4, 3 * fx["out_err32"]), d.max().item()
+    elif precision == "fp16":
+        assert d.max().item() <= 5e-3 and d.mean().item() <= 5e-4, (d.max().item(), d.mean().item())
     else:
         assert d.max().item() <= 3e-2 and d.mean().item() <= 3e-3, (d.max().item(), d.mean().item())
     assert abs(_psnr([o.detach() for o in out] if isinstance(out, list) else out.detach(), hr).item()
                - fx["psnr_acdc"]) <= 0.01
     for key, ref in fx["running_stats"].items():  # BatchNorm running statistics after the step
         got_rs = net.state_dict()[key].detach().cpu().double()
-        assert (got_rs - ref.double()).abs().max().item() <= (1e-5 if precision == "fp32" else 2e-2) * (
+        assert (got_rs - ref.double()).abs().max().item() <= {"fp32": 1e-5, "fp16": 3e-3}.get(precision, 2e-2) * (
             1 + ref.double().abs().max().item()), key
     gmax = fx["grad_max64"]
     for k, p in net.named_parameters():
         g = p.grad.detach().cpu().double()
         r32 = fx["ref32_err"][k]
         if r32 is None:  # exact gradient is zero
-            assert g.norm().item() <= (1e-4 if precision == "fp32" else 2e-2) * gmax, (k, g.norm().item())
+            assert g.norm().item() <= {"fp32": 1e-4, "fp16": 3e-3}.get(precision, 2e-2) * gmax, (k, g.norm().item())
             continue
         rel = _rel(g, fx, k)
         if precision == "fp32":
             tol = 1e-4 if name in COND else max(1e-4, 3 * r32)
+        elif precision == "fp16":
+            # fp16 storage rounds 8x finer than bf16 (2^-11 vs 2^-8): the bf16
+            # envelope scaled by 1/8, doubled as for bf16
+            tol = max(1e-2, fx["bf16_env"][k] / 4, 3 * r32)
         else:
             tol = max(8e-2, 2 * fx["bf16_env"][k])
         assert rel <= tol, (k, rel, tol)

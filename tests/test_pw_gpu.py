@@ -19,8 +19,8 @@ DEV = "cuda"
 BF = torch.bfloat16
 
 
-def _q(t):
-    return t.to(BF).double()
+def _q(t, dt=BF):
+    return t.to(dt).double()
 
 
 def _ref1x1(x_cl, w, b):
@@ -175,3 +175,33 @@ def test_pw_matches_tile_kernels(c):
     for a_, b_ in zip(res[0], res[1]):
         # bf16 outputs may differ by one rounding step; fp32 gradients by summation order
         assert (a_ - b_).abs().max().item() <= 1e-2 * (1 + b_.abs().max().item())
+
+
+@pytest.mark.parametrize("c", [64, 160, 256])
+def test_pw_fp16_forward_and_weight_gradient(c):
+    """fp16 instantiation (v_mfma_f32_32x32x16_f16): forward with prologue into
+    a channel slice, and the weight gradient; 11-bit rounding -> 2e-3 bounds."""
+    H = torch.float16
+    g = torch.Generator().manual_seed(3 * c)
+    n, d, h, w = 2, 2, 8, 32
+    big = torch.randn((n, d, h, w, c + 16), generator=g)
+    wt = torch.randn((c, c), generator=g) / c ** 0.5
+    b = torch.randn(c, generator=g)
+    sc = torch.rand(c, generator=g) + 0.5
+    sh = torch.randn(c, generator=g)
+    xin = torch.relu(_q(big[..., 8:8 + c], H) * sc.double() + sh.double()).to(H).double()
+    ref = _ref1x1(xin, _q(wt, H), b.double())
+    y = torch.empty((n, d, h, w, c), dtype=H, device=DEV)
+    bigd = big.to(DEV, H)
+    F.conv(bigd[..., 8:8 + c], F.pack_weight(wt.view(c, c, 1, 1, 1).to(DEV), 0, H), y, (1, 1, 1), (0, 0, 0),
+           bias=b.to(DEV), prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV))
+    err = (y.double().cpu() - ref).abs().max().item()
+    assert err <= 2e-3 * ref.abs().max().item(), err
+    gy = torch.randn((n, d, h, w, c), generator=g)
+    ref_w = torch.einsum("ndhwo,ndhwc->oc", _q(gy, H), xin)
+    dw = torch.empty((c, c, 1, 1, 1), device=DEV)
+    db = torch.empty(c, device=DEV)
+    F.conv_wgrad(bigd[..., 8:8 + c], gy.to(DEV, H), (1, 1, 1), (0, 0, 0), dw, db, prologue=F.PRO_AFFINE_RELU,
+                 pro_scale=sc.to(DEV), pro_shift=sh.to(DEV))
+    ew = (dw.view(c, c).double().cpu() - ref_w).abs().max().item()
+    assert ew <= 2e-3 * (1 + ref_w.abs().max().item()), ew

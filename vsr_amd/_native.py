@@ -17,10 +17,11 @@ from . import build as _build
 
 VSRK_F32 = 0
 VSRK_BF16 = 1
+VSRK_F16 = 2
 PRO_NONE, PRO_RELU, PRO_AFFINE, PRO_AFFINE_RELU = 0, 1, 2, 3
 ACT_NONE, ACT_RELU, ACT_PRELU = 0, 1, 2
 
-_DTYPE = {torch.float32: VSRK_F32, torch.bfloat16: VSRK_BF16}
+_DTYPE = {torch.float32: VSRK_F32, torch.bfloat16: VSRK_BF16, torch.float16: VSRK_F16}
 
 
 class Tensor5(C.Structure):
@@ -150,7 +151,7 @@ def dtype_code(dt: torch.dtype) -> int:
     try:
         return _DTYPE[dt]
     except KeyError:
-        raise TypeError(f"vsrk supports float32/bfloat16 activations, got {dt}") from None
+        raise TypeError(f"vsrk supports float32/bfloat16/float16 activations, got {dt}") from None
 
 
 def t5(t: torch.Tensor, shuffle: int = 1) -> Tensor5:

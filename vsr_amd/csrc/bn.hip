@@ -313,7 +313,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(View x, View y, const flo
 int reduce_launch(int mode, const vsrk_tensor5* x, const vsrk_tensor5* dz, const float* scale, const float* shift,
                   const float* mean, const float* invstd, float* o1, float* o2, void* ws, size_t ws_bytes,
                   hipStream_t s) {
-  const int E = x->dtype == VSRK_BF16 ? 8 : 4;
+  const int E = vsrk_is16(x->dtype) ? 8 : 4;
   const int cpv = ceil_div(x->c, E);
   VSRK_CHECK(cpv <= 256, "bn: too many channels (%d)", x->c);
   const int vpb = 256 / cpv;
@@ -334,6 +334,9 @@ int reduce_launch(int mode, const vsrk_tensor5* x, const vsrk_tensor5* dz, const
   if (x->dtype == VSRK_BF16) {
     if (mode == 0) chan_reduce_kernel<bf16, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
     else chan_reduce_kernel<bf16, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
+  } else if (x->dtype == VSRK_F16) {
+    if (mode == 0) chan_reduce_kernel<f16, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
+    else chan_reduce_kernel<f16, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
   } else {
     if (mode == 0) chan_reduce_kernel<float, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
     else chan_reduce_kernel<float, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
@@ -392,7 +395,7 @@ extern "C" int vsrk_bn_relu_bwd_apply(const vsrk_tensor5* x, const vsrk_tensor5*
   VSRK_CHECK(x && dz && dx && scale && shift && mean && invstd && sum_dy && sum_dy_xhat, "bn_relu_bwd_apply: null");
   VSRK_CHECK(x->dtype == dz->dtype && x->dtype == dx->dtype && x->c == dz->c && x->c == dx->c,
              "bn_relu_bwd_apply: view mismatch");
-  const int E = x->dtype == VSRK_BF16 ? 8 : 4;
+  const int E = vsrk_is16(x->dtype) ? 8 : 4;
   const int cpv = ceil_div(x->c, E);
   VSRK_CHECK(cpv <= 256, "bn_relu_bwd_apply: too many channels (%d)", x->c);
   VSRK_CHECK(dz->n == x->n && dz->d == x->d && dz->h == x->h && dz->w == x->w && dx->n == x->n &&
@@ -409,6 +412,10 @@ extern "C" int vsrk_bn_relu_bwd_apply(const vsrk_tensor5* x, const vsrk_tensor5*
     bn_relu_bwd_apply_kernel<bf16><<<grid, thr, 0, s>>>(make_view(x), make_view(dz), make_view(dx), scale, shift,
                                                         mean, invstd, gamma, sum_dy, sum_dy_xhat,
                                                         (float)(1.0 / count), nrows, accumulate);
+  else if (x->dtype == VSRK_F16)
+    bn_relu_bwd_apply_kernel<f16><<<grid, thr, 0, s>>>(make_view(x), make_view(dz), make_view(dx), scale, shift,
+                                                        mean, invstd, gamma, sum_dy, sum_dy_xhat,
+                                                        (float)(1.0 / count), nrows, accumulate);
   else
     bn_relu_bwd_apply_kernel<float><<<grid, thr, 0, s>>>(make_view(x), make_view(dz), make_view(dx), scale, shift,
                                                          mean, invstd, gamma, sum_dy, sum_dy_xhat,
@@ -423,7 +430,7 @@ extern "C" int vsrk_bn_apply(const vsrk_tensor5* x, const float* scale, const fl
   VSRK_CHECK(x->dtype == y->dtype && x->c == y->c && x->n == y->n && x->d == y->d && x->h == y->h && x->w == y->w &&
                  x->shuffle <= 1 && y->shuffle <= 1,
              "bn_apply: view mismatch");
-  const int E = x->dtype == VSRK_BF16 ? 8 : 4;
+  const int E = vsrk_is16(x->dtype) ? 8 : 4;
   const int cpv = ceil_div(x->c, E);
   VSRK_CHECK(cpv <= 256, "bn_apply: too many channels (%d)", x->c);
   const int64_t nr64 = (int64_t)x->n * x->d * x->h;
@@ -435,6 +442,8 @@ extern "C" int vsrk_bn_apply(const vsrk_tensor5* x, const float* scale, const fl
   hipStream_t s = (hipStream_t)stream;
   if (x->dtype == VSRK_BF16)
     bn_apply_kernel<bf16><<<grid, thr, 0, s>>>(make_view(x), make_view(y), scale, shift, relu, nrows);
+  else if (x->dtype == VSRK_F16)
+    bn_apply_kernel<f16><<<grid, thr, 0, s>>>(make_view(x), make_view(y), scale, shift, relu, nrows);
   else
     bn_apply_kernel<float><<<grid, thr, 0, s>>>(make_view(x), make_view(y), scale, shift, relu, nrows);
   VSRK_LAUNCH_CHECK("bn_apply");

@@ -138,6 +138,11 @@ __device__ __forceinline__ void mma<bf16>(f32x16& acc, uint4 a, uint4 b) {
                                                 __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
 }
 template <>
+__device__ __forceinline__ void mma<f16>(f32x16& acc, uint4 a, uint4 b) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), acc, 0,
+                                               0, 0);
+}
+template <>
 __device__ __forceinline__ void mma<float>(f32x16& acc, uint4 a, uint4 b) {
   // lane half hf supplies k = 4*hf + j for MFMA j on both operands, so the
   // four k=2 products cover the 8 channels of the slice exactly once.
@@ -186,8 +191,8 @@ __device__ __forceinline__ void load4(const char* base, int64_t off, bool vec, i
       v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
     } else {
       uint2 t = *reinterpret_cast<const uint2*>(p);
-      const bf16* b = reinterpret_cast<const bf16*>(&t);
-      for (int e = 0; e < 4; ++e) v[e] = (float)b[e];
+      const YT* b = reinterpret_cast<const YT*>(&t);
+      for (int e = 0; e < 4; ++e) v[e] = to_f32<YT>(b[e]);
     }
   } else {
     for (int e = 0; e < 4; ++e) v[e] = e < valid ? to_f32<YT>(p[e]) : 0.f;

@@ -65,7 +65,7 @@ int vsrk_conv_fwd_fast(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
     g_fast_mode = (e && e[0] == '0') ? 0 : 1;
   }
   if (g_fast_mode == 0) return 0;
-  if (x->dtype != VSRK_BF16) return 0;
+  if (!vsrk_is16(x->dtype)) return 0;
   if (const int k3 = vsrk_conv_fwd_k3(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s)) return k3;
   if (!chunk_ok(x, 2) || x->c % 8 != 0) return 0;
   const int xr = x->shuffle > 1 ? x->shuffle : 1, yr = y->shuffle > 1 ? y->shuffle : 1;
@@ -74,7 +74,7 @@ int vsrk_conv_fwd_fast(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   if (xr > 1 && d->prologue) return 0;
   if (d->kh != d->kw || (d->kh != 1 && d->kh != 3)) return 0;
   // every 4-channel output group stored with one 8/16-byte access
-  const int ye = y->dtype == VSRK_BF16 ? 2 : 4;
+  const int ye = vsrk_esize(y->dtype);
   if (((uintptr_t)y->ptr) % (4 * ye) != 0 || y->sn % 4 || y->sd % 4 || y->sh % 4 || y->sw % 4) return 0;
   if (y->c % 4 != 0 && !(y->c < 4 && !residual && !mask && !d->accumulate)) return 0;
   for (const vsrk_tensor5* t : {residual, mask}) {
@@ -93,7 +93,7 @@ int vsrk_conv_fwd_fast(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   a.y = make_view(y);
   a.res = residual ? make_view(residual) : a.y;
   a.msk = mask ? make_view(mask) : a.y;
-  a.w = (const bf16*)w_packed;
+  a.w = w_packed;
   a.bias = bias;
   a.pro_scale = pro_scale;
   a.pro_shift = pro_shift;
@@ -115,20 +115,21 @@ int vsrk_conv_fwd_fast(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   const int NT = y->c <= 32 ? 32 : (y->c <= 64 || d->kh == 3) ? 64 : 128;
   a.ntn = ceil_div(y->c, NT);
   const bool yf = y->dtype == VSRK_F32;
+  const bool h16 = x->dtype == VSRK_F16;
   const bool ys = yr > 1, xs = xr > 1;
   int rc;
   if (d->kh == 1) {
     if (xs || ys) return 0;  // not instantiated (never requested)
-    rc = fast_k1(a, NT, yf, s);
+    rc = fast_k1(a, NT, yf, h16, s);
   } else if (NT == 32) {
     if (xs || ys) return 0;
-    rc = fast_k3_n32(a, yf, s);
+    rc = fast_k3_n32(a, yf, h16, s);
   } else if (!xs && !ys) {
-    rc = fast_k3_n64(a, yf, s);
+    rc = fast_k3_n64(a, yf, h16, s);
   } else if (xs && !ys) {
-    rc = fast_k3_n64_xs(a, yf, s);
+    rc = fast_k3_n64_xs(a, yf, h16, s);
   } else if (!xs && ys) {
-    rc = fast_k3_n64_ys(a, yf, s);
+    rc = fast_k3_n64_ys(a, yf, h16, s);
   } else {
     return 0;
   }

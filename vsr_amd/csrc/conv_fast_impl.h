@@ -40,7 +40,7 @@ namespace vsrk_conv {
 
 struct FastArgs {
   View x, y, res, msk;
-  const bf16* w;
+  const void* w;  // packed weight, elements of the input's 16-bit type
   const float* bias;
   const float* pro_scale;
   const float* pro_shift;
@@ -62,11 +62,11 @@ int fast_grid(int64_t ntiles);
 
 // Per-family launchers (one translation unit each).  Return VSRK_OK, an error
 // status, or kFastNotEligible when the shape does not fit the family's LDS.
-int fast_k1(const FastArgs& a, int nt, bool yf, hipStream_t s);       // conv_fast_k1.hip
-int fast_k3_n32(const FastArgs& a, bool yf, hipStream_t s);           // conv_fast_k3_n32.hip
-int fast_k3_n64(const FastArgs& a, bool yf, hipStream_t s);           // conv_fast_k3_n64.hip
-int fast_k3_n64_xs(const FastArgs& a, bool yf, hipStream_t s);        // conv_fast_k3_n64_xs.hip
-int fast_k3_n64_ys(const FastArgs& a, bool yf, hipStream_t s);        // conv_fast_k3_n64_ys.hip
+int fast_k1(const FastArgs& a, int nt, bool yf, bool h16, hipStream_t s);       // conv_fast_k1.hip
+int fast_k3_n32(const FastArgs& a, bool yf, bool h16, hipStream_t s);           // conv_fast_k3_n32.hip
+int fast_k3_n64(const FastArgs& a, bool yf, bool h16, hipStream_t s);           // conv_fast_k3_n64.hip
+int fast_k3_n64_xs(const FastArgs& a, bool yf, bool h16, hipStream_t s);        // conv_fast_k3_n64_xs.hip
+int fast_k3_n64_ys(const FastArgs& a, bool yf, bool h16, hipStream_t s);        // conv_fast_k3_n64_ys.hip
 
 }  // namespace vsrk_conv
 
@@ -79,7 +79,7 @@ __device__ __attribute__((aligned(256))) uint4 g_zero_page[16];
 
 
 
-template <int KK, int NT, int MS, int XS, int YS, int PRO, typename YT, int NW>
+template <int KK, int NT, int MS, int XS, int YS, int PRO, typename YT, int NW, typename H>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(FastArgs a) {
   constexpr int NTH = NW * 64;
   constexpr int NS = NT / 32;
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
   constexpr int NAW = (NAI + NW - 1) / NW;
   constexpr int NBW = (NBI + NW - 1) / NW;
   static_assert(NAW <= 16 && NBW <= 16, "per-wave DMA count");
-  // transposed epilogue (bf16 output): channel block CB and where its
+  // transposed epilogue (H output): channel block CB and where its
   // per-wave scratch lives -- in the ring slot that is idle at epilogue
   // time, or (small slots) in a region of its own after the ring.
   constexpr bool TRANS = sizeof(YT) == 2;
@@ -203,8 +203,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
   // prep() resolves the stage's base addresses and the lane's chunk
   // validity, dma(q) issues this wave's q-th instruction (A chunks first).
   struct Dma {
-    const bf16* xb;
-    const bf16* wsrc;
+    const H* xb;
+    const H* wsrc;
     uint32_t sbase;
     unsigned m;  // valid A chunks of this lane (bit k)
     bool on;
@@ -234,8 +234,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
     } else {
       xoff = tl.nb * a.x.sn + (int64_t)(dok ? di : 0) * a.x.sd + (int64_t)hb * a.x.sh + (int64_t)wb * a.x.sw + c0;
     }
-    d.xb = reinterpret_cast<const bf16*>(a.x.ptr) + xoff;
-    d.wsrc = a.w + ((int64_t)kdi * TAPS * a.cout_pad + tl.n0) * a.cin_pad + c0;
+    d.xb = reinterpret_cast<const H*>(a.x.ptr) + xoff;
+    d.wsrc = reinterpret_cast<const H*>(a.w) + ((int64_t)kdi * TAPS * a.cout_pad + tl.n0) * a.cin_pad + c0;
     d.sbase = lds_addr(lds) + slot * SLOT;
     d.m = 0;
 #pragma unroll
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
     for (int k = 0; k < NAW; ++k) {
       if ((m >> k) & 1) {
         uint4* p = reinterpret_cast<uint4*>(lds + slot * SLOT + (wave + NW * k) * 1024 + lane * 16);
-        *p = prologue_lds<bf16>(*p, c0 + a_p8[k], relu_in, lsc, lsh);
+        *p = prologue_lds<H>(*p, c0 + a_p8[k], relu_in, lsc, lsh);
       }
     }
   };
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
 #pragma unroll
         for (int ms = 0; ms < MS; ++ms)
 #pragma unroll
-          for (int ns = 0; ns < NS; ++ns) mma<bf16>(acc[ms][ns], f.bw[kh][ns], f.ax[ms + kh]);
+          for (int ns = 0; ns < NS; ++ns) mma<H>(acc[ms][ns], f.bw[kh][ns], f.ax[ms + kh]);
       if (d.on) {
 #pragma unroll
         for (int q = it * QPG; q < (it + 1) * QPG; ++q) dma(d, q);
@@ -431,7 +431,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[m][n][i] = 0.f;
   };
-  // Transposed epilogue (bf16 output): per (row ms, block of CB channels)
+  // Transposed epilogue (H output): per (row ms, block of CB channels)
   // each wave parks its raw fp32 accumulators in a private LDS scratch
   // [32 voxels][CB] (rows padded 16 B: conflict-free b128 writes), reads
   // them back as (voxel, 8 consecutive channels) per lane and finishes
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
 #pragma unroll
         for (int cbk = 0; cbk < PNB; ++cbk) {
           const int co = tl.n0 + cbk * CB + (lane % PLPV) * 8;
-          const bf16* rowp = reinterpret_cast<const bf16*>(pv.ptr) +
+          const H* rowp = reinterpret_cast<const H*>(pv.ptr) +
                              (tl.nb * pv.sn + (int64_t)tl.dz * pv.sd + (int64_t)ho * pv.sh + co);
 #pragma unroll
           for (int st = 0; st < PNST; ++st) {
@@ -528,37 +528,37 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
             t[e] = fmaf(t[e], osc, bsv[e]);
             if (act) t[e] = act_apply(a.act, t[e], aslope);
           }
-          bf16* yp = reinterpret_cast<bf16*>(a.y.ptr) + yrow + (int64_t)wo * yr * a.y.sw;
+          H* yp = reinterpret_cast<H*>(a.y.ptr) + yrow + (int64_t)wo * yr * a.y.sw;
           if ((MODE & 2) && use_msk) {
-            const bf16* mp = reinterpret_cast<const bf16*>(a.msk.ptr) + (tl.nb * a.msk.sn + (int64_t)tl.dz * a.msk.sd +
+            const H* mp = reinterpret_cast<const H*>(a.msk.ptr) + (tl.nb * a.msk.sn + (int64_t)tl.dz * a.msk.sd +
                                                                            (int64_t)ho * a.msk.sh + (int64_t)wo * a.msk.sw + co);
             uint4 mv;
             if constexpr (USE_PRE) mv = pre[ms][cbk][st];
             else mv = ok ? *reinterpret_cast<const uint4*>(mp) : make_uint4(0, 0, 0, 0);
             float m[8];
-            Chunk<bf16>::unpack(mv, m);
+            Chunk<H>::unpack(mv, m);
 #pragma unroll
             for (int e = 0; e < 8; ++e) t[e] = mask_apply(m[e], t[e], mslope);
           }
           if ((MODE & 1) && use_res) {
-            const bf16* rp = reinterpret_cast<const bf16*>(a.res.ptr) + (tl.nb * a.res.sn + (int64_t)tl.dz * a.res.sd +
+            const H* rp = reinterpret_cast<const H*>(a.res.ptr) + (tl.nb * a.res.sn + (int64_t)tl.dz * a.res.sd +
                                                                            (int64_t)ho * a.res.sh + (int64_t)wo * a.res.sw + co);
             uint4 rv;
             if constexpr (USE_PRE) rv = pre[ms][cbk][st];
             else rv = ok ? *reinterpret_cast<const uint4*>(rp) : make_uint4(0, 0, 0, 0);
             float rr[8];
-            Chunk<bf16>::unpack(rv, rr);
+            Chunk<H>::unpack(rv, rr);
 #pragma unroll
             for (int e = 0; e < 8; ++e) t[e] += rr[e];
           }
           if ((MODE & 4) && use_acc) {
             const uint4 ov = ok ? *reinterpret_cast<const uint4*>(yp) : make_uint4(0, 0, 0, 0);
             float o[8];
-            Chunk<bf16>::unpack(ov, o);
+            Chunk<H>::unpack(ov, o);
 #pragma unroll
             for (int e = 0; e < 8; ++e) t[e] += o[e];
           }
-          if (ok) *reinterpret_cast<uint4*>(yp) = Chunk<bf16>::pack(t);
+          if (ok) *reinterpret_cast<uint4*>(yp) = Chunk<H>::pack(t);
         }
       }
     }
@@ -651,7 +651,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
 }
 
 
-template <int KK, int NT, int MS, int XS, int YS, int PRO, typename YT, int NW>
+template <int KK, int NT, int MS, int XS, int YS, int PRO, typename YT, int NW, typename H>
 int launch_fast(FastArgs a, hipStream_t s) {
   constexpr int FTH = NW * MS;
   constexpr int HWd = TW + KK - 1;
@@ -668,7 +668,7 @@ int launch_fast(FastArgs a, hipStream_t s) {
   const size_t lds = 2 * (size_t)SLOT + (SCR_OWN ? NW * 32 * (CB * 4 + 16) : 0) + (size_t)a.cout_pad * 4 +
                      (PRO ? 2 * (size_t)a.cin_pad * 4 : 0);
   if (lds > 160 * 1024) return kFastNotEligible;  // e.g. a 4096-entry bias table: generic kernel
-  auto kern = conv_fast_kernel<KK, NT, MS, XS, YS, PRO, YT, NW>;
+  auto kern = conv_fast_kernel<KK, NT, MS, XS, YS, PRO, YT, NW, H>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int grid = fast_grid(ntiles);
   kern<<<grid, NW * 64, lds, s>>>(a);
@@ -676,15 +676,17 @@ int launch_fast(FastArgs a, hipStream_t s) {
   return VSRK_OK;
 }
 
-template <int KK, int NT, int MS, int XS, int YS, typename YT, int NW = 8>
+template <int KK, int NT, int MS, int XS, int YS, typename YT, typename H, int NW = 8>
 int fast_pro(const FastArgs& a, hipStream_t s) {
-  if (a.prologue) return launch_fast<KK, NT, MS, XS, YS, 1, YT, NW>(a, s);
-  return launch_fast<KK, NT, MS, XS, YS, 0, YT, NW>(a, s);
+  if (a.prologue) return launch_fast<KK, NT, MS, XS, YS, 1, YT, NW, H>(a, s);
+  return launch_fast<KK, NT, MS, XS, YS, 0, YT, NW, H>(a, s);
 }
 
+// y in fp32 or in the input's 16-bit type H (bf16 / fp16)
 template <int KK, int NT, int MS, int XS, int YS>
-int fast_y(const FastArgs& a, bool yf, hipStream_t s) {
-  return yf ? fast_pro<KK, NT, MS, XS, YS, float>(a, s) : fast_pro<KK, NT, MS, XS, YS, bf16>(a, s);
+int fast_y(const FastArgs& a, bool yf, bool h16, hipStream_t s) {
+  if (h16) return yf ? fast_pro<KK, NT, MS, XS, YS, float, f16>(a, s) : fast_pro<KK, NT, MS, XS, YS, f16, f16>(a, s);
+  return yf ? fast_pro<KK, NT, MS, XS, YS, float, bf16>(a, s) : fast_pro<KK, NT, MS, XS, YS, bf16, bf16>(a, s);
 }
 }  // namespace
 #endif  // VSRK_FAST_KERNEL_TU

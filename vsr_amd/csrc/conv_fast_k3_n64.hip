@@ -3,4 +3,4 @@
 #define VSRK_FAST_KERNEL_TU
 #include "conv_fast_impl.h"
 
-int vsrk_conv::fast_k3_n64(const FastArgs& a, bool yf, hipStream_t s) { return fast_y<3, 64, 2, 0, 0>(a, yf, s); }
+int vsrk_conv::fast_k3_n64(const FastArgs& a, bool yf, bool h16, hipStream_t s) { return fast_y<3, 64, 2, 0, 0>(a, yf, h16, s); }

@@ -4,4 +4,4 @@
 #define VSRK_FAST_KERNEL_TU
 #include "conv_fast_impl.h"
 
-int vsrk_conv::fast_k3_n64_ys(const FastArgs& a, bool yf, hipStream_t s) { return fast_y<3, 64, 2, 0, 1>(a, yf, s); }
+int vsrk_conv::fast_k3_n64_ys(const FastArgs& a, bool yf, bool h16, hipStream_t s) { return fast_y<3, 64, 2, 0, 1>(a, yf, h16, s); }

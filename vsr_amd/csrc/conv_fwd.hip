@@ -389,6 +389,9 @@ extern "C" int vsrk_conv_pack_weight(int32_t dtype, const float* w, int32_t cout
   if (dtype == VSRK_BF16)
     pack_weight_kernel<bf16><<<grid, blk, 0, s>>>(w, (bf16*)packed, cout, cin, kd, kh, kw, mode, perm_r,
                                                   co_pad, ci_pad, total);
+  else if (dtype == VSRK_F16)
+    pack_weight_kernel<f16><<<grid, blk, 0, s>>>(w, (f16*)packed, cout, cin, kd, kh, kw, mode, perm_r,
+                                                 co_pad, ci_pad, total);
   else
     pack_weight_kernel<float><<<grid, blk, 0, s>>>(w, (float*)packed, cout, cin, kd, kh, kw, mode, perm_r,
                                                    co_pad, ci_pad, total);
@@ -459,9 +462,9 @@ extern "C" int vsrk_conv_fwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, con
                              void* stream) {
   VSRK_CHECK(d && x && y && w_packed, "conv_fwd: null argument");
   const int xdt = x->dtype, ydt = y->dtype;
-  VSRK_CHECK(xdt == VSRK_F32 || xdt == VSRK_BF16, "conv_fwd: bad x dtype");
+  VSRK_CHECK(xdt == VSRK_F32 || vsrk_is16(xdt), "conv_fwd: bad x dtype");
   VSRK_CHECK(ydt == xdt || ydt == VSRK_F32, "conv_fwd: y dtype must equal x dtype or be f32");
-  const int es = xdt == VSRK_BF16 ? 2 : 4;
+  const int es = vsrk_esize(xdt);
   if (!view_ok(x, "conv_fwd x") || !view_ok(y, "conv_fwd y")) return VSRK_ERR_INVALID;
   VSRK_CHECK(d->kh == d->kw && (d->kh == 1 || d->kh == 3) && d->kd >= 1,
              "conv_fwd: kernel %dx%dx%d unsupported (kh = kw in {1, 3})", d->kd, d->kh, d->kw);
@@ -520,6 +523,10 @@ extern "C" int vsrk_conv_fwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, con
   if (xdt == VSRK_BF16) {
     if (ydt == VSRK_BF16) return dispatch_k<bf16, bf16>(a, NT, s);
     return dispatch_k<bf16, float>(a, NT, s);
+  }
+  if (xdt == VSRK_F16) {
+    if (ydt == VSRK_F16) return dispatch_k<f16, f16>(a, NT, s);
+    return dispatch_k<f16, float>(a, NT, s);
   }
   return dispatch_k<float, float>(a, NT, s);
 }

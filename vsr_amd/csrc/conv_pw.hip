@@ -1,4 +1,4 @@
-// Pointwise (1x1x1) convolution on CDNA4 for bf16 channels-last activations:
+// Pointwise (1x1x1) convolution on CDNA4 for 16-bit (bf16 / fp16) channels-last activations:
 // forward / data-gradient (pw_fwd) and weight gradient (pw_wgrad).
 //
 // DUF's dense-unit bottlenecks (BN3d-ReLU-Conv1x1x1, duf_net.py:198-200,
@@ -106,10 +106,11 @@ __device__ __forceinline__ void bstore8(Rsrc r, uint32_t off, uint2 v) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, v), r, (int)off, 0, 0);
 }
 
-__device__ __forceinline__ uint4 bf16x8_affine(uint4 v, const float4& s0, const float4& s1, const float4& h0,
-                                               const float4& h1, bool relu) {
+template <typename H>
+__device__ __forceinline__ uint4 h8_affine(uint4 v, const float4& s0, const float4& s1, const float4& h0,
+                                          const float4& h1, bool relu) {
   float f[8];
-  Chunk<bf16>::unpack(v, f);
+  Chunk<H>::unpack(v, f);
   const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
   const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
 #pragma unroll
@@ -117,14 +118,14 @@ __device__ __forceinline__ uint4 bf16x8_affine(uint4 v, const float4& s0, const 
     const float t = fmaf(f[e], sc[e], sh[e]);
     f[e] = relu ? fmaxf(t, 0.f) : t;
   }
-  return Chunk<bf16>::pack(f);
+  return Chunk<H>::pack(f);
 }
 
-struct PwArgs {
-  const bf16* x;
-  bf16* y;
-  const bf16* msk;
-  const bf16* w;  // packed [round_up(cout,128)][ci_pad] (vsrk_conv_pack_weight)
+struct PwArgs {  // 16-bit tensors of one type H (bf16 / fp16)
+  const void* x;
+  void* y;
+  const void* msk;
+  const void* w;  // packed [round_up(cout,128)][ci_pad] (vsrk_conv_pack_weight)
   const float* bias;
   const float* pro_scale;
   const float* pro_shift;
@@ -164,8 +165,12 @@ __device__ __forceinline__ uint32_t lane_off(const TileBase& tb, int k, int v, i
 // KS = 2*NCB k-steps of 16 input channels (cin_pad == 32*NCB), M tiles of 32
 // voxels per wave step.
 // ---------------------------------------------------------------------------
-template <int NCB, int M, bool PRO, bool EIN>
+template <int NCB, int M, bool PRO, bool EIN, typename H>
 __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
+  const H* aX = reinterpret_cast<const H*>(a.x);
+  H* aY = reinterpret_cast<H*>(a.y);
+  const H* aM = reinterpret_cast<const H*>(a.msk);
+  const H* aW = reinterpret_cast<const H*>(a.w);
   constexpr int KS = 2 * NCB;
   constexpr int COP = 32 * NCB;
   constexpr int CIP = 16 * KS;
@@ -183,7 +188,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
     const int ci = 16 * s + 8 * h;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (ci < a.ci_pad && co0 + co < a.co_rows)
-      v = *reinterpret_cast<const uint4*>(a.w + (int64_t)(co0 + co) * a.ci_pad + ci);
+      v = *reinterpret_cast<const uint4*>(aW + (int64_t)(co0 + co) * a.ci_pad + ci);
     *reinterpret_cast<uint4*>(lw + i * 16) = v;
   }
   if (PRO) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, CIP, tid, PW_THR);
@@ -199,7 +204,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
   auto load = [&](int tile, uint4 (&b)[M][KS]) __attribute__((always_inline)) {
     const int v0 = tile * 32 * M;
     const TileBase tb = tile_base(v0, a.fd);
-    const Rsrc r = rsrc_at(a.x + (int64_t)tb.n0 * a.xsn);
+    const Rsrc r = rsrc_at(aX + (int64_t)tb.n0 * a.xsn);
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const uint32_t off = lane_off(tb, m * 32 + col, v0 + m * 32 + col, a.nvox, a.fd, a.xsn, a.xsw);
@@ -218,12 +223,12 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
     const int tn = t + nwaves;
     const int v0 = t * 32 * M;
     const TileBase tb = tile_base(v0, a.fd);
-    const Rsrc ry = rsrc_at(a.y + (int64_t)tb.n0 * a.ysn);
+    const Rsrc ry = rsrc_at(aY + (int64_t)tb.n0 * a.ysn);
     // epilogue inputs of this tile first, then the next tile's operands: the
     // epilogue's wait (vmcnt) then leaves the prefetch in flight
     uint2 ein[EIN ? M : 1][NCB][4];
     if constexpr (EIN) {
-      const Rsrc rm = a.has_mask ? rsrc_at(a.msk + (int64_t)tb.n0 * a.msn) : ry;
+      const Rsrc rm = a.has_mask ? rsrc_at(aM + (int64_t)tb.n0 * a.msn) : ry;
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         const uint32_t off = a.has_mask
@@ -256,13 +261,13 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
           const float4 s0 = *reinterpret_cast<const float4*>(lsc + c), s1 = *reinterpret_cast<const float4*>(lsc + c + 4);
           const float4 h0 = *reinterpret_cast<const float4*>(lsh + c), h1 = *reinterpret_cast<const float4*>(lsh + c + 4);
 #pragma unroll
-          for (int m = 0; m < M; ++m) bc[m][s] = bf16x8_affine(bc[m][s], s0, s1, h0, h1, relu_in);
+          for (int m = 0; m < M; ++m) bc[m][s] = h8_affine<H>(bc[m][s], s0, s1, h0, h1, relu_in);
         }
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) {
           const uint4 af = *reinterpret_cast<const uint4*>(lw + ((s * 2 + hf) * COP + cb * 32 + col) * 16);
 #pragma unroll
-          for (int m = 0; m < M; ++m) mma<bf16>(acc[m][cb], af, bc[m][s]);
+          for (int m = 0; m < M; ++m) mma<H>(acc[m][cb], af, bc[m][s]);
         }
         // keep the scheduler from hoisting every k-step's weight reads (register pressure)
         __builtin_amdgcn_sched_barrier(0);
@@ -285,7 +290,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
           float o[4] = {acc[m][cb][4 * j] + bb.x, acc[m][cb][4 * j + 1] + bb.y, acc[m][cb][4 * j + 2] + bb.z,
                         acc[m][cb][4 * j + 3] + bb.w};
           float e4[4] = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (EIN) unpack_pk<bf16>(ein[m][cb][j], e4);
+          if constexpr (EIN) unpack_pk<H>(ein[m][cb][j], e4);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             float rr = act_apply(a.act, o[e] * a.out_scale, 0.f);
@@ -296,7 +301,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
           if (a.accumulate) {
             if (a.has_mask) {
               float y4[4];
-              unpack_pk<bf16>(bload8(ry, so), y4);
+              unpack_pk<H>(bload8(ry, so), y4);
 #pragma unroll
               for (int e = 0; e < 4; ++e) o[e] += y4[e];
             } else {
@@ -304,7 +309,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
               for (int e = 0; e < 4; ++e) o[e] += e4[e];
             }
           }
-          if (!(a.ablate & 1)) bstore8(ry, so, pack_pk<bf16, uint2>(o));
+          if (!(a.ablate & 1)) bstore8(ry, so, pack_pk<H, uint2>(o));
         }
       }
     }
@@ -319,18 +324,21 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
 }
 
 // Staged variant (no mask / accumulate, NCB <= 7): each wave owns an LDS
-// tile buffer [32*M voxels][CIP + 8 pad] bf16.  The next tile is fetched with
+// tile buffer [32*M voxels][CIP + 8 pad] H.  The next tile is fetched with
 // coalesced 16-byte loads (consecutive lanes -> consecutive bytes of a voxel
 // row, then the next row) into registers while the current tile computes; the
 // B fragments are read back from LDS (row pad: conflict-free ds_read_b128).
-// The outputs take the same way back: bf16-packed accumulators to the buffer,
+// The outputs take the same way back: H-packed accumulators to the buffer,
 // then coalesced 16-byte row stores.  Wave-private buffer: no barriers.
 // AL: every tile lies inside one sample (d*h*w % (32*M) == 0), so a voxel
 // row's offset is row * sw from the tile's base -- the common, cheap case;
 // otherwise rows are placed with a division per row.  ACT: VSRK_ACT_NONE /
 // VSRK_ACT_RELU at compile time (the epilogue is most of the VALU work).
-template <int NCB, int M, bool PRO, bool AL, int ACT>
+template <int NCB, int M, bool PRO, bool AL, int ACT, typename H>
 __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
+  const H* aX = reinterpret_cast<const H*>(a.x);
+  H* aY = reinterpret_cast<H*>(a.y);
+  const H* aW = reinterpret_cast<const H*>(a.w);
   constexpr int KS = 2 * NCB;
   constexpr int COP = 32 * NCB;
   constexpr int CIP = 16 * KS;
@@ -354,7 +362,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
     const int ci = 16 * s + 8 * h;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (ci < a.ci_pad && co0 + co < a.co_rows)
-      v = *reinterpret_cast<const uint4*>(a.w + (int64_t)(co0 + co) * a.ci_pad + ci);
+      v = *reinterpret_cast<const uint4*>(aW + (int64_t)(co0 + co) * a.ci_pad + ci);
     *reinterpret_cast<uint4*>(lw + i * 16) = v;
   }
   if (PRO) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, CIP, tid, PW_THR);
@@ -383,7 +391,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
     asm volatile("" : "+v"(ln));
     const int v0 = tile * ROWS;
     const TileBase tb = tile_base(v0, a.fd);
-    const Rsrc rs = rsrc_at(a.x + (int64_t)tb.n0 * a.xsn);
+    const Rsrc rs = rsrc_at(aX + (int64_t)tb.n0 * a.xsn);
 #pragma unroll
     for (int k = 0; k < NCK; ++k) {
       const int i = ln + 64 * k, row = i / CPR, c = 8 * (i % CPR);
@@ -449,15 +457,15 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
       if (s + 1 < KS) rd(s + 1, fr[(s + 1) & 1]);
       if (PRO) {
 #pragma unroll
-        for (int m = 0; m < M; ++m) f.b[m] = bf16x8_affine(f.b[m], f.s0, f.s1, f.h0, f.h1, relu_in);
+        for (int m = 0; m < M; ++m) f.b[m] = h8_affine<H>(f.b[m], f.s0, f.s1, f.h0, f.h1, relu_in);
       }
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
-        for (int m = 0; m < M; ++m) mma<bf16>(acc[m][cb], f.a[cb], f.b[m]);
+        for (int m = 0; m < M; ++m) mma<H>(acc[m][cb], f.a[cb], f.b[m]);
     }
 
-    // epilogue into the buffer (row = voxel, COP bf16 channels), then row stores
+    // epilogue into the buffer (row = voxel, COP H channels), then row stores
     {
       uint32_t ebase = lds_addr(buf) + col * RS + hf * 8;
       uint32_t bias_b = lds_addr(lb) + hf * 16;
@@ -476,14 +484,14 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
               o[e] *= osc;
               if constexpr (ACT == VSRK_ACT_RELU) o[e] = fmaxf(o[e], 0.f);
             }
-            lds_st8(ebase + m * 32 * RS + (cb * 32 + 8 * j) * 2, pack_pk<bf16, uint2>(o));
+            lds_st8(ebase + m * 32 * RS + (cb * 32 + 8 * j) * 2, pack_pk<H, uint2>(o));
           }
         }
     }
     {
       const int v0 = t * ROWS;
       const TileBase tb = tile_base(v0, a.fd);
-      const Rsrc ry = rsrc_at(a.y + (int64_t)tb.n0 * a.ysn);
+      const Rsrc ry = rsrc_at(aY + (int64_t)tb.n0 * a.ysn);
       constexpr int OCPR = COP / 8;
       constexpr int NOK = ROWS * OCPR / 64;
       int ln = lane;
@@ -506,8 +514,8 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
 // weight gradient
 // ---------------------------------------------------------------------------
 struct PwWArgs {
-  const bf16* x;
-  const bf16* dy;
+  const void* x;
+  const void* dy;
   const float* pro_scale;
   const float* pro_shift;
   float* ws;
@@ -522,11 +530,13 @@ struct PwWArgs {
 };
 
 // NCO dY channel blocks per chunk; wave w owns X blocks w, w+4 (NCIW of them).
-template <int NCO, int NCIW>
+template <int NCO, int NCIW, typename H>
 __global__ __launch_bounds__(PW_THR, 1) void pw_wgrad_kernel(PwWArgs a) {
+  const H* aX = reinterpret_cast<const H*>(a.x);
+  const H* aD = reinterpret_cast<const H*>(a.dy);
   constexpr int NCIMAX = 4 * NCIW;
   constexpr int PLMAX = NCO + NCIMAX;   // 32-channel planes per stage (max)
-  constexpr int PSZ = PW_KP * 64;       // bytes per plane: 64 voxel rows of 32 bf16
+  constexpr int PSZ = PW_KP * 64;       // bytes per plane: 64 voxel rows of 32 H
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int split = blockIdx.x, chunk = blockIdx.y;
@@ -570,8 +580,8 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_wgrad_kernel(PwWArgs a) {
   auto issue = [&](int st) __attribute__((always_inline)) {
     const int v0 = vbeg + st * PW_KP;
     const TileBase tb = tile_base(v0, a.fd);
-    const Rsrc rdy = rsrc_at(a.dy + (int64_t)tb.n0 * a.dsn);
-    const Rsrc rxx = rsrc_at(a.x + (int64_t)tb.n0 * a.xsn);
+    const Rsrc rdy = rsrc_at(aD + (int64_t)tb.n0 * a.dsn);
+    const Rsrc rxx = rsrc_at(aX + (int64_t)tb.n0 * a.xsn);
 #pragma unroll
     for (int k = 0; k < NCO; ++k) {
       const uint32_t off = lane_off(tb, dvox[k], v0 + dvox[k], vend, a.fd, a.dsn, a.dsw);
@@ -634,7 +644,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_wgrad_kernel(PwWArgs a) {
 #pragma unroll
     for (int kk = 0; kk < PW_KP / 16; ++kk) {
       const int row = kk * 16 + rowk;
-      bf16x8 bfr[NCIW];
+      uint4 bfr[NCIW];
 #pragma unroll
       for (int b = 0; b < NCIW; ++b) {
         const int blk = wave + 4 * b;
@@ -644,30 +654,32 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_wgrad_kernel(PwWArgs a) {
           uint4 xv = __builtin_bit_cast(uint4, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
           if (a.prologue) {
             float f[8];
-            Chunk<bf16>::unpack(xv, f);
+            Chunk<H>::unpack(xv, f);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float tt = fmaf(f[e], psc[b], psh[b]);
               f[e] = relu_in ? fmaxf(tt, 0.f) : tt;
             }
-            xv = Chunk<bf16>::pack(f);
+            xv = Chunk<H>::pack(f);
           }
-          bfr[b] = __builtin_bit_cast(bf16x8, xv);
+          bfr[b] = xv;
         }
       }
 #pragma unroll
       for (int cb = 0; cb < NCO; ++cb) {
         const char* py = base + cb * PSZ + row * 64 + colb;
         const v4i16 y0 = ds_read_tr(py), y1 = ds_read_tr(py + 4 * 64);
-        const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7));
+        const uint4 af = __builtin_bit_cast(uint4, __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7));
         if (do_bias) {
+          float fa[8];
+          Chunk<H>::unpack(af, fa);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) bsum[cb] += (float)af[e];
+          for (int e = 0; e < 8; ++e) bsum[cb] += fa[e];
         }
 #pragma unroll
         for (int b = 0; b < NCIW; ++b)
           if (wave + 4 * b < a.ncit)
-            acc[cb][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr[b], acc[cb][b], 0, 0, 0);
+            mma<H>(acc[cb][b], af, bfr[b]);
       }
     }
     if (st + 1 < nst) commit((st + 1) & 1);
@@ -761,7 +773,7 @@ static bool dhw_dense(const vsrk_tensor5* t) {
          (t->d == 1 || t->sd == (int64_t)t->h * t->sh);
 }
 
-template <int NCB, int M>
+template <int NCB, int M, typename H>
 static void launch_fwd(const PwArgs& a, int nchunk, bool pro, hipStream_t s) {
   constexpr int KS = 2 * NCB, COP = 32 * NCB, CIP = 16 * KS;
   int grid = (int)std::min<int64_t>(pw_num_cus(), ceil_div64(a.ntiles, PW_THR / 64));
@@ -782,11 +794,11 @@ static void launch_fwd(const PwArgs& a, int nchunk, bool pro, hipStream_t s) {
       using K = void (*)(PwArgs);
       K kern;
       if (pro) {
-        if (al) kern = relu ? pw_fwd_staged_kernel<NCB, M, true, true, 1> : pw_fwd_staged_kernel<NCB, M, true, true, 0>;
-        else kern = relu ? pw_fwd_staged_kernel<NCB, M, true, false, 1> : pw_fwd_staged_kernel<NCB, M, true, false, 0>;
+        if (al) kern = relu ? pw_fwd_staged_kernel<NCB, M, true, true, 1, H> : pw_fwd_staged_kernel<NCB, M, true, true, 0, H>;
+        else kern = relu ? pw_fwd_staged_kernel<NCB, M, true, false, 1, H> : pw_fwd_staged_kernel<NCB, M, true, false, 0, H>;
       } else {
-        if (al) kern = relu ? pw_fwd_staged_kernel<NCB, M, false, true, 1> : pw_fwd_staged_kernel<NCB, M, false, true, 0>;
-        else kern = relu ? pw_fwd_staged_kernel<NCB, M, false, false, 1> : pw_fwd_staged_kernel<NCB, M, false, false, 0>;
+        if (al) kern = relu ? pw_fwd_staged_kernel<NCB, M, false, true, 1, H> : pw_fwd_staged_kernel<NCB, M, false, true, 0, H>;
+        else kern = relu ? pw_fwd_staged_kernel<NCB, M, false, false, 1, H> : pw_fwd_staged_kernel<NCB, M, false, false, 0, H>;
       }
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       kern<<<dim3(grid, nchunk), PW_THR, lds, s>>>(a);
@@ -794,8 +806,8 @@ static void launch_fwd(const PwArgs& a, int nchunk, bool pro, hipStream_t s) {
     }
   }
   const size_t lds = (size_t)KS * 2 * COP * 16 + (2 * CIP + COP) * sizeof(float);
-  auto kern = pro ? (ein ? pw_fwd_kernel<NCB, M, true, true> : pw_fwd_kernel<NCB, M, true, false>)
-                  : (ein ? pw_fwd_kernel<NCB, M, false, true> : pw_fwd_kernel<NCB, M, false, false>);
+  auto kern = pro ? (ein ? pw_fwd_kernel<NCB, M, true, true, H> : pw_fwd_kernel<NCB, M, true, false, H>)
+                  : (ein ? pw_fwd_kernel<NCB, M, false, true, H> : pw_fwd_kernel<NCB, M, false, false, H>);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   kern<<<dim3(grid, nchunk), PW_THR, lds, s>>>(a);
 }
@@ -811,11 +823,11 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
                      const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                      const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s) {
   if (!pw_enabled()) return 0;
-  if (x->dtype != VSRK_BF16 || y->dtype != VSRK_BF16) return 0;
+  if (!vsrk_is16(x->dtype) || y->dtype != x->dtype) return 0;
   if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->pd || d->ph || d->pw) return 0;
   if (residual || d->act == VSRK_ACT_PRELU || d->bias_perm_r > 1) return 0;
   if (x->n != y->n || x->d != y->d || x->h != y->h || x->w != y->w) return 0;
-  if (!dhw_dense(x) || !dhw_dense(y) || (mask && (!dhw_dense(mask) || mask->dtype != VSRK_BF16))) return 0;
+  if (!dhw_dense(x) || !dhw_dense(y) || (mask && (!dhw_dense(mask) || mask->dtype != x->dtype))) return 0;
   if (mask && (mask->n != y->n || mask->d != y->d || mask->h != y->h || mask->w != y->w || mask->c != y->c)) return 0;
   if (x->c % 8 || y->c % 4 || !chunk_ok(x, 2)) return 0;
   if (((uintptr_t)y->ptr) % 8 || y->sn % 4 || y->sw % 4) return 0;
@@ -827,10 +839,10 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
   if (cop_total % cip != 0) return 0;  // output handled in chunks of CIP channels
   const int nchunk = cop_total / cip;
   PwArgs a;
-  a.x = (const bf16*)x->ptr;
-  a.y = (bf16*)y->ptr;
-  a.msk = mask ? (const bf16*)mask->ptr : nullptr;
-  a.w = (const bf16*)w_packed;
+  a.x = x->ptr;
+  a.y = y->ptr;
+  a.msk = mask ? mask->ptr : nullptr;
+  a.w = w_packed;
   a.bias = bias;
   a.pro_scale = pro_scale;
   a.pro_shift = pro_shift;
@@ -872,7 +884,10 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
 #define PW_CASE(N)                                                     \
   case N:                                                              \
     a.ntiles = ceil_div(a.nvox, 32 * pw_m<N>());                       \
-    launch_fwd<N, pw_m<N>()>(a, nchunk, pro, s);                       \
+    vsrk_dispatch16(x->dtype, [&](auto tag) {                          \
+      launch_fwd<N, pw_m<N>(), decltype(tag)>(a, nchunk, pro, s);      \
+      return 0;                                                        \
+    });                                                                \
     break;
     PW_CASE(2) PW_CASE(3) PW_CASE(4) PW_CASE(5) PW_CASE(6) PW_CASE(7) PW_CASE(8)
 #undef PW_CASE
@@ -899,7 +914,7 @@ PwWPlan pw_wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk
   PwWPlan p{};
   p.ok = false;
   if (!pw_enabled()) return p;
-  if (x->dtype != VSRK_BF16 || dy->dtype != VSRK_BF16) return p;
+  if (!vsrk_is16(x->dtype) || dy->dtype != x->dtype) return p;
   if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->pd || d->ph || d->pw) return p;
   if (x->n != dy->n || x->d != dy->d || x->h != dy->h || x->w != dy->w) return p;
   if (!dhw_dense(x) || !dhw_dense(dy) || !chunk_ok(x, 2) || !chunk_ok(dy, 2)) return p;
@@ -934,10 +949,10 @@ PwWPlan pw_wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk
   return p;
 }
 
-template <int NCO, int NCIW>
+template <int NCO, int NCIW, typename H>
 void launch_wgrad_pw(const PwWArgs& a, int nsplit, hipStream_t s) {
   const size_t lds = (size_t)2 * (NCO + 4 * NCIW) * PW_KP * 64;
-  auto kern = pw_wgrad_kernel<NCO, NCIW>;
+  auto kern = pw_wgrad_kernel<NCO, NCIW, H>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   kern<<<dim3(nsplit, a.nchunks), PW_THR, lds, s>>>(a);
 }
@@ -960,8 +975,8 @@ int vsrk_conv_wgrad_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsr
     return -VSRK_ERR_INVALID;
   }
   PwWArgs a;
-  a.x = (const bf16*)x->ptr;
-  a.dy = (const bf16*)dy->ptr;
+  a.x = x->ptr;
+  a.dy = dy->ptr;
   a.pro_scale = pro_scale;
   a.pro_shift = pro_shift;
   a.ws = (float*)workspace;
@@ -984,7 +999,12 @@ int vsrk_conv_wgrad_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsr
     switch (p.nco) {
 #define PWW_CASE(N)                                                                   \
   case N:                                                                             \
-    if (w2) launch_wgrad_pw<N, 2>(a, p.nsplit, s); else launch_wgrad_pw<N, 1>(a, p.nsplit, s); \
+    vsrk_dispatch16(x->dtype, [&](auto tag) {                                       \
+      using H = decltype(tag);                                                      \
+      if (w2) launch_wgrad_pw<N, 2, H>(a, p.nsplit, s);                            \
+      else launch_wgrad_pw<N, 1, H>(a, p.nsplit, s);                               \
+      return 0;                                                                     \
+    });                                                                             \
     break;
       PWW_CASE(2) PWW_CASE(3) PWW_CASE(4) PWW_CASE(5) PWW_CASE(6) PWW_CASE(7) PWW_CASE(8)
 #undef PWW_CASE

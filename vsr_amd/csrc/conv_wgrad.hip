@@ -176,7 +176,7 @@ __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) vo
         const int vrow = vb / TW, vcol0 = (vb % TW) + 8 * hfk;
         v4i16 y0 = ds_read_tr(py + (vrow * TW + vcol0 + q) * PB + colb);
         v4i16 y1 = ds_read_tr(py + (vrow * TW + vcol0 + 4 + q) * PB + colb);
-        bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7));
+        const uint4 af = __builtin_bit_cast(uint4, __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
         for (int khi = 0; khi < KK; ++khi) {
 #pragma unroll
@@ -184,8 +184,8 @@ __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) vo
             const char* xs = px + ((vrow + khi) * HWd + vcol0 + kwi + q) * PB + colb;
             v4i16 x0 = ds_read_tr(xs);
             v4i16 x1 = ds_read_tr(xs + 4 * PB);
-            bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
-            acc[khi * KK + kwi] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[khi * KK + kwi], 0, 0, 0);
+            const uint4 bfr = __builtin_bit_cast(uint4, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+            mma<T>(acc[khi * KK + kwi], af, bfr);
           }
         }
       }
@@ -412,7 +412,7 @@ extern "C" int vsrk_conv_wgrad(const vsrk_conv_desc* d, const vsrk_tensor5* x, c
                                size_t workspace_bytes, void* stream) {
   VSRK_CHECK(d && x && dy && dw, "conv_wgrad: null argument");
   VSRK_CHECK(x->dtype == dy->dtype, "conv_wgrad: x/dy dtype mismatch");
-  const int es = x->dtype == VSRK_BF16 ? 2 : 4;
+  const int es = vsrk_esize(x->dtype);
   if (!view_ok(x, "conv_wgrad x") || !view_ok(dy, "conv_wgrad dy")) return VSRK_ERR_INVALID;
   VSRK_CHECK(d->kh == d->kw && (d->kh == 1 || d->kh == 3), "conv_wgrad: kh = kw in {1, 3}");
   VSRK_CHECK(!(d->prologue & VSRK_PRO_AFFINE) || (pro_scale && pro_shift), "conv_wgrad: affine prologue needs scale/shift");
@@ -455,11 +455,15 @@ extern "C" int vsrk_conv_wgrad(const vsrk_conv_desc* d, const vsrk_tensor5* x, c
     // thin-channel kernel (conv_thin.hip), same slab layout
   } else if (x->dtype == VSRK_BF16 && vec && vsrk_conv_wgrad_fast(a, p.nco, p.nci, s)) {
     // LDS-DMA kernel (conv_wgrad_fast.hip), same slab layout
-  } else if (x->dtype == VSRK_BF16) {
-    if (p.nco == 2 && p.nci == 2) wgrad_k<bf16, 2, 2>(a, vec, s);
-    else if (p.nco == 2) wgrad_k<bf16, 2, 1>(a, vec, s);
-    else if (p.nci == 2) wgrad_k<bf16, 1, 2>(a, vec, s);
-    else wgrad_k<bf16, 1, 1>(a, vec, s);
+  } else if (vsrk_is16(x->dtype)) {
+    vsrk_dispatch16(x->dtype, [&](auto tag) {
+      using H = decltype(tag);
+      if (p.nco == 2 && p.nci == 2) wgrad_k<H, 2, 2>(a, vec, s);
+      else if (p.nco == 2) wgrad_k<H, 2, 1>(a, vec, s);
+      else if (p.nci == 2) wgrad_k<H, 1, 2>(a, vec, s);
+      else wgrad_k<H, 1, 1>(a, vec, s);
+      return 0;
+    });
   } else {
     wgrad_k<float, 1, 1>(a, vec, s);
   }

@@ -196,6 +196,8 @@ extern "C" int vsrk_prelu_wgrad(const vsrk_tensor5* y, const vsrk_tensor5* dx, c
   double* part = (double*)workspace;
   if (y->dtype == VSRK_BF16)
     prelu_partial_kernel<bf16><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vd, nvox, part);
+  else if (y->dtype == VSRK_F16)
+    prelu_partial_kernel<f16><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vd, nvox, part);
   else
     prelu_partial_kernel<float><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vd, nvox, part);
   VSRK_LAUNCH_CHECK("prelu_partial");
@@ -306,8 +308,8 @@ extern "C" int vsrk_prelu_bwd(const vsrk_tensor5* y, const vsrk_tensor5* dy, con
   const View vg2 = dy2 ? make_view(dy2) : vg;
   const int64_t nr64 = (int64_t)y->n * y->d * y->h;
   VSRK_CHECK(nr64 < (1ll << 31), "prelu_bwd: too many rows");
-  VSRK_CHECK(ceil_div(y->c, y->dtype == VSRK_BF16 ? 8 : 4) <= 256, "prelu_bwd: too many channels (%d)", y->c);
-  const int esz = y->dtype == VSRK_BF16 ? 2 : 4, E = 16 / esz;
+  VSRK_CHECK(ceil_div(y->c, vsrk_is16(y->dtype) ? 8 : 4) <= 256, "prelu_bwd: too many channels (%d)", y->c);
+  const int esz = vsrk_esize(y->dtype), E = 16 / esz;
   int vec = 1;
   for (const vsrk_tensor5* t : {y, dy, dy2, dx}) {
     if (!t) continue;
@@ -317,6 +319,8 @@ extern "C" int vsrk_prelu_bwd(const vsrk_tensor5* y, const vsrk_tensor5* dy, con
   double* part = (double*)workspace;
   if (y->dtype == VSRK_BF16)
     prelu_bwd_kernel<bf16><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, (int)nr64, vec, part);
+  else if (y->dtype == VSRK_F16)
+    prelu_bwd_kernel<f16><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, (int)nr64, vec, part);
   else
     prelu_bwd_kernel<float><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, (int)nr64, vec, part);
   VSRK_LAUNCH_CHECK("prelu_bwd");

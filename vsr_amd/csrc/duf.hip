@@ -110,6 +110,9 @@ extern "C" int vsrk_duf_dynfilter_bwd(const float* x, const float* logits, const
   if (grad_dtype == VSRK_BF16)
     launch_duf<true, bf16>(size_filter, total, s, x, logits, nullptr, nullptr, grad_out, (bf16*)grad_logits,
                            (bf16*)grad_residual, n, h, w, upscale);
+  else if (grad_dtype == VSRK_F16)
+    launch_duf<true, f16>(size_filter, total, s, x, logits, nullptr, nullptr, grad_out, (f16*)grad_logits,
+                           (f16*)grad_residual, n, h, w, upscale);
   else
     launch_duf<true, float>(size_filter, total, s, x, logits, nullptr, nullptr, grad_out, (float*)grad_logits,
                             (float*)grad_residual, n, h, w, upscale);

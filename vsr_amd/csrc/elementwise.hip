@@ -252,7 +252,7 @@ __global__ void psnr_final_kernel(const double* __restrict__ part, int batch, in
 }  // namespace
 
 // ---------------------------------------------------------------------------
-static inline int esize(int dt) { return dt == VSRK_BF16 ? 2 : 4; }
+static inline int esize(int dt) { return vsrk_esize(dt); }
 static inline int64_t nvox(const vsrk_tensor5* t) { return (int64_t)t->n * t->d * t->h * t->w; }
 
 size_t vsrk_channel_reduce_ws_bytes(int c) { return (size_t)RED_BLOCKS * 2 * c * sizeof(float); }
@@ -267,6 +267,8 @@ int vsrk_channel_reduce_internal(const vsrk_tensor5* x, int mode, int perm_r, fl
   float* part = (float*)ws;
   if (x->dtype == VSRK_BF16)
     channel_partial_kernel<bf16><<<nblk, 256, 0, s>>>(v, nv, mode, part);
+  else if (x->dtype == VSRK_F16)
+    channel_partial_kernel<f16><<<nblk, 256, 0, s>>>(v, nv, mode, part);
   else
     channel_partial_kernel<float><<<nblk, 256, 0, s>>>(v, nv, mode, part);
   VSRK_LAUNCH_CHECK("channel_partial");
@@ -285,7 +287,7 @@ extern "C" int vsrk_ncdhw_to_view(const float* src, int32_t n, int32_t c, int32_
   const int64_t total = nvox(dst) * dst->c;
   hipStream_t s = (hipStream_t)stream;
   const int64_t cp = dst->c, dhw = (int64_t)d * h * w;
-  const int esz = dst->dtype == VSRK_BF16 ? 2 : 4;
+  const int esz = vsrk_esize(dst->dtype);
   const bool dense = dst->shuffle <= 1 && dst->sw == cp && dst->sh == w * cp && dst->sd == h * dst->sh &&
                      dst->sn == d * dst->sd && (cp * esz) % 16 == 0 && ((uintptr_t)dst->ptr) % 16 == 0 &&
                      nvox(dst) < (1ll << 31) && dhw * c < (1ll << 31);
@@ -293,6 +295,8 @@ extern "C" int vsrk_ncdhw_to_view(const float* src, int32_t n, int32_t c, int32_
     const int nv = (int)nvox(dst);
     if (dst->dtype == VSRK_BF16)
       ncdhw_to_dense_kernel<bf16><<<ceil_div(nv, 256), 256, 0, s>>>(src, c, (int)dhw, (int)cp, nv, (bf16*)dst->ptr);
+    else if (dst->dtype == VSRK_F16)
+      ncdhw_to_dense_kernel<f16><<<ceil_div(nv, 256), 256, 0, s>>>(src, c, (int)dhw, (int)cp, nv, (f16*)dst->ptr);
     else
       ncdhw_to_dense_kernel<float><<<ceil_div(nv, 256), 256, 0, s>>>(src, c, (int)dhw, (int)cp, nv, (float*)dst->ptr);
     VSRK_LAUNCH_CHECK("ncdhw_to_view(dense)");
@@ -300,6 +304,8 @@ extern "C" int vsrk_ncdhw_to_view(const float* src, int32_t n, int32_t c, int32_
   }
   if (dst->dtype == VSRK_BF16)
     ncdhw_to_view_kernel<bf16><<<(int)ceil_div64(total, 256), 256, 0, s>>>(src, n, c, d, h, w, v, total);
+  else if (dst->dtype == VSRK_F16)
+    ncdhw_to_view_kernel<f16><<<(int)ceil_div64(total, 256), 256, 0, s>>>(src, n, c, d, h, w, v, total);
   else
     ncdhw_to_view_kernel<float><<<(int)ceil_div64(total, 256), 256, 0, s>>>(src, n, c, d, h, w, v, total);
   VSRK_LAUNCH_CHECK("ncdhw_to_view");
@@ -314,6 +320,8 @@ extern "C" int vsrk_view_to_ncdhw(const vsrk_tensor5* src, float* dst, int32_t c
   hipStream_t s = (hipStream_t)stream;
   if (src->dtype == VSRK_BF16)
     view_to_ncdhw_kernel<bf16><<<(int)ceil_div64(total, 256), 256, 0, s>>>(v, dst, c, total);
+  else if (src->dtype == VSRK_F16)
+    view_to_ncdhw_kernel<f16><<<(int)ceil_div64(total, 256), 256, 0, s>>>(v, dst, c, total);
   else
     view_to_ncdhw_kernel<float><<<(int)ceil_div64(total, 256), 256, 0, s>>>(v, dst, c, total);
   VSRK_LAUNCH_CHECK("view_to_ncdhw");
@@ -327,6 +335,8 @@ extern "C" int vsrk_relu_bwd(const vsrk_tensor5* y, const vsrk_tensor5* dy, cons
   hipStream_t s = (hipStream_t)stream;
   if (y->dtype == VSRK_BF16)
     relu_bwd_kernel<bf16><<<(int)ceil_div64(total, 256), 256, 0, s>>>(make_view(y), make_view(dy), make_view(dx), total);
+  else if (y->dtype == VSRK_F16)
+    relu_bwd_kernel<f16><<<(int)ceil_div64(total, 256), 256, 0, s>>>(make_view(y), make_view(dy), make_view(dx), total);
   else
     relu_bwd_kernel<float><<<(int)ceil_div64(total, 256), 256, 0, s>>>(make_view(y), make_view(dy), make_view(dx), total);
   VSRK_LAUNCH_CHECK("relu_bwd");
@@ -340,6 +350,8 @@ extern "C" int vsrk_add(const vsrk_tensor5* a, const vsrk_tensor5* b, const vsrk
   hipStream_t s = (hipStream_t)stream;
   if (a->dtype == VSRK_BF16)
     add_kernel<bf16><<<(int)ceil_div64(total, 256), 256, 0, s>>>(make_view(a), make_view(b), make_view(out), total);
+  else if (a->dtype == VSRK_F16)
+    add_kernel<f16><<<(int)ceil_div64(total, 256), 256, 0, s>>>(make_view(a), make_view(b), make_view(out), total);
   else
     add_kernel<float><<<(int)ceil_div64(total, 256), 256, 0, s>>>(make_view(a), make_view(b), make_view(out), total);
   VSRK_LAUNCH_CHECK("add");
@@ -369,6 +381,8 @@ extern "C" int vsrk_loss_bwd(int32_t kind, float param, const float* out, const 
   hipStream_t s = (hipStream_t)stream;
   if (grad_dtype == VSRK_BF16)
     loss_bwd_kernel<bf16><<<nblk, 256, 0, s>>>(kind, param, out, target, count, gscale, (bf16*)grad);
+  else if (grad_dtype == VSRK_F16)
+    loss_bwd_kernel<f16><<<nblk, 256, 0, s>>>(kind, param, out, target, count, gscale, (f16*)grad);
   else
     loss_bwd_kernel<float><<<nblk, 256, 0, s>>>(kind, param, out, target, count, gscale, (float*)grad);
   VSRK_LAUNCH_CHECK("loss_bwd");

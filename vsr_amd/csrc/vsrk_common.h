@@ -7,6 +7,8 @@
 
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -32,9 +34,11 @@ void vsrk_set_error(const char* fmt, ...);
 template <typename T> __device__ __forceinline__ float to_f32(T v);
 template <> __device__ __forceinline__ float to_f32<float>(float v) { return v; }
 template <> __device__ __forceinline__ float to_f32<bf16>(bf16 v) { return (float)v; }
+template <> __device__ __forceinline__ float to_f32<f16>(f16 v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T from_f32(float v);
 template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
 template <> __device__ __forceinline__ bf16 from_f32<bf16>(float v) { return (bf16)v; }
+template <> __device__ __forceinline__ f16 from_f32<f16>(float v) { return (f16)v; }
 
 // 16-byte chunk <-> float lanes.  A chunk holds 8 bf16 or 4 f32 channels.
 template <typename T> struct Chunk;
@@ -50,6 +54,21 @@ template <> struct Chunk<bf16> {
     bf16* p = reinterpret_cast<bf16*>(&v);
 #pragma unroll
     for (int i = 0; i < 8; ++i) p[i] = (bf16)f[i];
+    return v;
+  }
+};
+template <> struct Chunk<f16> {
+  static constexpr int E = 8;
+  __device__ static inline void unpack(uint4 v, float* f) {
+    const f16* p = reinterpret_cast<const f16*>(&v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = (float)p[i];
+  }
+  __device__ static inline uint4 pack(const float* f) {
+    uint4 v;
+    f16* p = reinterpret_cast<f16*>(&v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) p[i] = (f16)f[i];
     return v;
   }
 };
@@ -98,4 +117,16 @@ __device__ __forceinline__ int64_t view_off(const View& v, int n, int d, int h, 
   int cc = c - sub * v.cphys;
   int i = sub / v.r, j = sub - (sub / v.r) * v.r;
   return n * v.sn + d * v.sd + (int64_t)(h * v.r + i) * v.sh + (int64_t)(w * v.r + j) * v.sw + cc;
+}
+
+// ---- host-side dtype helpers ----
+// 16-bit storage types (bf16, fp16) share every kernel family; the MFMA
+// flavour follows the type (v_mfma_f32_32x32x16_bf16 / _f16).
+static inline bool vsrk_is16(int dt) { return dt == VSRK_BF16 || dt == VSRK_F16; }
+static inline int vsrk_esize(int dt) { return dt == VSRK_F32 ? 4 : 2; }
+// Call f(tag) with a value of the 16-bit element type of dtype dt.
+template <typename Fn>
+static inline auto vsrk_dispatch16(int dt, Fn&& f) {
+  if (dt == VSRK_F16) return f(f16{});
+  return f(bf16{});
 }

@@ -76,10 +76,12 @@ class GradSync:
         for b, h in enumerate(self._handles):
             if h is None:
                 self._launch(b)
+        unscale = getattr(self.net, "_grad_unscale", 1.0)  # fp16 loss scale (BaseNet._loss_scale)
         for b, h in enumerate(self._handles):
             self._handles[b].wait()
-            if not self._avg:
-                self.flat[b].mul_(1.0 / self.world)
+            f = unscale if self._avg else unscale / self.world
+            if f != 1.0:
+                self.flat[b].mul_(f)
         self._reset()
         self._attach()
 

@@ -11,8 +11,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-_COMPUTE_DTYPES = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32,
-                   "float32": torch.float32}
+_COMPUTE_DTYPES = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp16": torch.float16,
+                   "float16": torch.float16, "fp32": torch.float32, "float32": torch.float32}
 
 
 class BaseNet(nn.Module):
@@ -22,6 +22,8 @@ class BaseNet(nn.Module):
         super().__init__()
         self.compute_dtype = torch.bfloat16
         self._grad_sink = None  # vsr_amd.ddp.GradSync when data-parallel
+        # fp16 loss scale: None = automatic (see _loss_scale), else a fixed float
+        self.loss_scale = None
 
     # -- gradient plumbing used by the subclasses' backward passes ----------
     def _grad_buffer(self, p: torch.Tensor) -> torch.Tensor:
@@ -39,10 +41,32 @@ class BaseNet(nn.Module):
         else:
             grads[id(p)] = g
 
-    def set_precision(self, precision: str) -> "BaseNet":
-        """'bf16' (bf16 activations, fp32 master weights/accumulation) or 'fp32'."""
+    def set_precision(self, precision: str, loss_scale: float | None = None) -> "BaseNet":
+        """'bf16' or 'fp16' (16-bit activations and data gradients, fp32 master
+        weights, fp32 accumulation and fp32 weight gradients) or 'fp32'.  fp16
+        backward passes run loss-scaled (see _loss_scale); loss_scale fixes
+        the factor instead."""
         self.compute_dtype = _COMPUTE_DTYPES[precision]
+        self.loss_scale = loss_scale
         return self
+
+    def _loss_scale(self, grads) -> float:
+        """Factor the output gradient is multiplied by before an fp16 backward
+        (and every parameter gradient divided by after it) -- the static
+        counterpart of torch.cuda.amp.GradScaler.  The reference's losses are
+        means over the output (losses.py:5-34, nn.L1Loss/MSELoss), so the
+        output gradient is O(1/N) for N output elements: below fp16's normal
+        range (6.1e-5) at N > 16k, and the data gradients of early layers sit
+        further down in fp16's subnormals, where fewer significant bits remain.
+        Automatic scale: 2^floor(log2 N), i.e. output gradients in [1, 2).  bf16
+        / fp32: 1."""
+        if self.compute_dtype != torch.float16:
+            return 1.0
+        if self.loss_scale is not None:
+            return float(self.loss_scale)
+        gs = grads if isinstance(grads, (tuple, list)) else (grads,)
+        n = sum(g.numel() for g in gs if g is not None)
+        return float(2 ** max(0, max(n, 1).bit_length() - 1))
 
     def __repr__(self):
         n = sum(p.numel() for p in self.parameters() if p.requires_grad)
@@ -84,6 +108,14 @@ class _TapeFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
-        g = ctx.net._backward(ctx.tape, grads if len(grads) > 1 else grads[0])
+        net = ctx.net
+        scale = net._loss_scale(grads)
+        if scale != 1.0:
+            grads = tuple(g * scale if g is not None else None for g in grads)
+        net._grad_unscale = 1.0 / scale
+        g = net._backward(ctx.tape, grads if len(grads) > 1 else grads[0])
         ctx.tape = None
+        if scale != 1.0 and net._grad_sink is None:
+            for t in g.values():
+                t.mul_(1.0 / scale)  # the data-parallel path unscales in GradSync.finish
         return (None, None, *[g.get(id(p)) for p in ctx.params])
