@@ -122,24 +122,33 @@ def _psnr(out, target, dataset="acdc"):
     return cpu_nets.psnr(cpu_nets.denormalize(out, dataset), cpu_nets.denormalize(target, dataset))
 
 
-def _bf16_envelope(cls, kwargs, lr64, hr64, g64, ref32_err, seed, draws=4):
-    """Gradient error of an ideal bf16-storage implementation: fp64 math with
-    bf16 conv weights and every conv / BatchNorm output, its input gradient
-    and the network input rounded to bf16 (dithered so each draw rounds
-    differently).  Worst rel-L2 over draws per parameter; the bf16 parity
-    bound of the HIP path is a multiple of this."""
+def _bf16_envelope(cls, kwargs, lr64, hr64, g64, ref32_err, seed, draws=4, dtype=torch.bfloat16):
+    """Gradient error of an ideal 16-bit-storage implementation (bf16, or
+    fp16 with dtype=torch.float16): fp64 math with 16-bit conv weights and
+    every conv / BatchNorm output, its input gradient and the network input
+    rounded to the 16-bit type (dithered so each draw rounds differently).
+    Worst rel-L2 over draws per parameter; the 16-bit parity bound of the HIP
+    path is a multiple of this."""
+    dither = 2.0 ** -12 if dtype == torch.bfloat16 else 2.0 ** -15
+    # fp16 gradients run loss-scaled, as the HIP path does (BaseNet._loss_scale:
+    # 2^floor(log2 N) for N output elements); bf16 has fp32's range: unscaled
+    n_out = sum(t.numel() for t in hr64) if isinstance(hr64, list) else hr64.numel()
+    gscale = float(2 ** (n_out.bit_length() - 1)) if dtype == torch.float16 else 1.0
     env = {k: (0.0 if v is not None else None) for k, v in ref32_err.items()}
     for draw in range(draws):
         g = torch.Generator().manual_seed(seed + 100 + draw)
 
         def q(t):
-            d = t + t.abs() * 2.0 ** -12 * torch.randn(t.shape, generator=g, dtype=t.dtype)
-            return d.to(torch.bfloat16).to(t.dtype)
+            d = t + t.abs() * dither * torch.randn(t.shape, generator=g, dtype=t.dtype)
+            return d.to(dtype).to(t.dtype)
+
+        def qg(t):
+            return q(t * gscale) / gscale
 
         def hook(mod, inp, out):
             out = out + (q(out.detach()) - out.detach())  # straight-through rounding
             if out.requires_grad:
-                out.register_hook(q)
+                out.register_hook(qg)
             return out
 
         torch.manual_seed(seed)
@@ -147,7 +156,7 @@ def _bf16_envelope(cls, kwargs, lr64, hr64, g64, ref32_err, seed, draws=4):
         with torch.no_grad():
             for mod in m.modules():
                 if isinstance(mod, torch.nn.modules.conv._ConvNd):
-                    mod.weight.copy_(mod.weight.to(torch.bfloat16).double())
+                    mod.weight.copy_(mod.weight.to(dtype).double())
         for mod in m.modules():
             if isinstance(mod, (torch.nn.modules.conv._ConvNd, torch.nn.modules.batchnorm._BatchNorm)):
                 mod.register_forward_hook(hook)
