@@ -416,3 +416,39 @@ def test_thin_matches_generic(case):
             F.set_conv_path("thin", -1)
     for a_, b_ in zip(outs[0], outs[1]):
         assert (a_ - b_).abs().max().item() <= 1e-4 * (1 + b_.abs().max().item())
+
+
+@pytest.mark.parametrize("case", THIN_FWD)
+def test_thin_conv_fp16(case):
+    """fp16 instantiation of the thin-channel kernels (forward and, for the
+    cout <= 3 cases, the weight gradient) against fp64."""
+    n, d, h, w, ci, co, k, pad, padded = case
+    H = torch.float16
+    g = torch.Generator().manual_seed(27)
+    x = torch.randn((n, d, h, w, ci), generator=g)
+    wt = torch.randn((co, ci, *k), generator=g) / (ci * k[0] * k[1] * k[2]) ** 0.5
+    b = torch.randn(co, generator=g)
+    do = d + 2 * pad[0] - k[0] + 1
+    ref = _ref_conv(_q(x, H), _q(wt, H), b.double(), pad)
+    if ci < 8 and padded:
+        xs = torch.zeros((*x.shape[:-1], 8), dtype=H, device=DEV)
+        xs[..., :ci] = x.to(DEV, H)
+        xd = xs[..., :ci]
+    else:
+        xd = x.to(DEV, H)
+    y = torch.empty((n, do, h, w, co), dtype=torch.float32, device=DEV)
+    F.conv(xd, F.pack_weight(wt.to(DEV), 0, H), y, k, pad, bias=b.to(DEV))
+    err = (y.double().cpu() - ref).abs().max().item()
+    assert err <= _tol(H, ref), err
+    if co <= 3 and ci % 8 == 0 and k[0] == 1:
+        gy = torch.randn((n, do, h, w, co), generator=g)
+        gys = torch.zeros((n, do, h, w, 8), dtype=H, device=DEV)
+        gys[..., :co] = gy.to(DEV, H)
+        wr = _q(wt, H).requires_grad_(True)
+        br = torch.zeros(co, dtype=torch.float64, requires_grad=True)
+        _ref_conv(_q(x, H), wr, br, pad).backward(_q(gy, H))
+        dw = torch.empty((co, ci, *k), device=DEV)
+        db = torch.empty(co, device=DEV)
+        F.conv_wgrad(x.to(DEV, H), gys[..., :co], k, pad, dw, db)
+        ew = (dw.double().cpu() - wr.grad).abs().max().item()
+        assert ew <= 2e-3 * (1 + wr.grad.abs().max().item()), ew

@@ -23,15 +23,16 @@ fp32 HIP path: output max |d| <= max(1e-4, 3*out_err32); gradient rel-L2 <=
   Parameters whose exact gradient is 0 (conv biases feeding a BatchNorm):
   |g| <= 1e-4 * max gradient norm.
 fp16 HIP path (loss-scaled backward, BaseNet._loss_scale): output max |d| <=
-  5e-3, mean <= 5e-4; gradient rel-L2 <= max(3e-2, 2*fp16_env), fp16_env the
+  5e-3, mean <= 5e-4; gradient rel-L2 <= max(3e-2, 3*fp16_env), fp16_env the
   ideal fp16-storage envelope (as bf16_env, with fp16 rounding of the
   loss-scaled gradients; oracle/add_fp16_env.py).  It is not 8x below
   bf16_env everywhere: a 16-bit rounding of an activation near zero flips
   its mask whatever the significand width (DRF in_block: 3.9e-2 for both the
   ideal fp16 model and the HIP path).  The 3e-2 floor is measured, not
-  derived: on EDSR the HIP fp16 path sits at up to 2.6e-2 (body / head
-  weights) where the ideal model predicts < 2e-3, against 5e-2 in bf16;
-  unexplained so far (loss scale from 1 to 2^18 does not move it).
+  derived: on edsr_x4_small the HIP fp16 path sits at 1.7e-2 on one weight
+  where the 4-draw ideal model predicts 6e-4 (5e-2 in bf16; loss scale 1 to
+  2^18 does not move it); on edsr_x4_canon it tracks the envelope (2-3e-2 vs
+  1.5-3e-2, tools/diag/f16_edsr.py), hence the 3x multiplier.
 bf16 HIP path: output max |d| <= 3e-2, mean |d| <= 3e-3; gradient rel-L2 <=
   max(8e-2, 2*bf16_env) where bf16_env is the error of an *ideal*
   bf16-storage implementation (fp64 math, bf16 weights, every conv/BN output
@@ -163,7 +164,7 @@ def test_net_matches_golden(name, precision):
         if precision == "fp32":
             tol = 1e-4 if name in COND else max(1e-4, 3 * r32)
         elif precision == "fp16":
-            tol = max(3e-2, 2 * fx["fp16_env"][k])
+            tol = max(3e-2, 3 * fx["fp16_env"][k])
         else:
             tol = max(8e-2, 2 * fx["bf16_env"][k])
         assert rel <= tol, (k, rel, tol)

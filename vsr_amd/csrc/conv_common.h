@@ -152,6 +152,18 @@ __device__ __forceinline__ void mma<float>(f32x16& acc, uint4 a, uint4 b) {
   acc = __builtin_amdgcn_mfma_f32_32x32x2f32(__builtin_bit_cast(float, a.w), __builtin_bit_cast(float, b.w), acc, 0, 0, 0);
 }
 
+// 8-element 16-bit MFMA operand vectors per element type, and the matching
+// v_mfma_f32_32x32x16_{bf16,f16}
+template <typename H> struct V8;
+template <> struct V8<bf16> { typedef bf16x8 type; };
+template <> struct V8<f16> { typedef f16x8 type; };
+__device__ __forceinline__ f32x16 mfma32x16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma32x16(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
 // 4 consecutive channels of an epilogue tensor, kept packed (uint2 for bf16,
 // uint4 for fp32) between the batched loads and the stores.
 template <typename YT, typename Pk>
@@ -243,7 +255,7 @@ static inline bool chunk_ok(const vsrk_tensor5* t, int esize) {
 // slab kernel, 0 = not eligible (use conv_wgrad_kernel).
 int vsrk_conv_wgrad_fast(const vsrk_conv::WgradArgs& a, int nco, int nci, hipStream_t s);
 // thin-channel weight gradient (conv_thin.hip): 1 = launched the slab kernel, 0 = not eligible.
-int vsrk_conv_wgrad_thin(const vsrk_conv::WgradArgs& a, int nco, int nci, int perm_r, hipStream_t s);
+int vsrk_conv_wgrad_thin(const vsrk_conv::WgradArgs& a, int nco, int nci, int perm_r, int dtype, hipStream_t s);
 
 static inline bool view_ok(const vsrk_tensor5* t, const char* what) {
   if (!t || !t->ptr) {

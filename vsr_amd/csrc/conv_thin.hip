@@ -38,7 +38,7 @@ constexpr int NPW = 4;           // thin wgrad: dY patch elements per thread (co
 
 struct ThinArgs {
   View x, y, res, msk;
-  const bf16* w;  // packed [kd][kh][kw][cout_pad][cin_pad]
+  const void* w;  // packed [kd][kh][kw][cout_pad][cin_pad], the input's 16-bit type
   const float* bias;
   const float* pro_scale;
   const float* pro_shift;
@@ -135,7 +135,7 @@ __device__ __forceinline__ int64_t corner(const View& v, int nb, int d, int h, i
 // 16-byte channel chunks.  Every per-thread index (patch slot, epilogue chunk)
 // is fixed for the launch and precomputed as an offset from the tile corner,
 // so a tile costs one 64-bit corner per tensor.
-template <typename YT, int KS, int NCBM>
+template <typename YT, int KS, int NCBM, typename H>
 __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(KS * NCBM <= 2 ? 3 : 2))) void conv_thin_in_kernel(
     ThinArgs a) {
   constexpr int E = 16 / (int)sizeof(YT);
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(KS * NCBM <
   constexpr int NIT = 256 * NCH / THR;  // epilogue chunks per thread and block
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float* lout = reinterpret_cast<float*>(lds);                  // [256][OROW]
-  bf16* patch = reinterpret_cast<bf16*>(lds + 256 * OROW * 4);  // [cin][kd][HH][WW]
+  H* patch = reinterpret_cast<H*>(lds + 256 * OROW * 4);  // [cin][kd][HH][WW]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n = lane & 31, hf = lane >> 5;
   const int HH = TH + a.kh - 1, WW = TWT + a.kw - 1;
   const int K = a.kd * a.kh * a.kw * a.cin;
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(KS * NCBM <
       }
     }
   // weights: A[co][k] = w[tap][co][c]
-  bf16x8 afr[NCBM][KS];
+  typename V8<H>::type afr[NCBM][KS];
 #pragma unroll
   for (int cb = 0; cb < NCBM; ++cb)
 #pragma unroll
@@ -177,10 +177,10 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(KS * NCBM <
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int k = 16 * s + 8 * hf + j, co = cb * 32 + n;
-        bf16 v = (bf16)0.f;
+        H v = (H)0.f;
         if (cb < ncb && k < K) {
           const int c = k % a.cin, tap = k / a.cin;
-          v = a.w[((int64_t)tap * a.cout_pad + co) * a.cin_pad + c];  // zero-padded past cout
+          v = reinterpret_cast<const H*>(a.w)[((int64_t)tap * a.cout_pad + co) * a.cin_pad + c];  // zero-padded past cout
         }
         afr[cb][s][j] = v;
       }
@@ -212,15 +212,15 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(KS * NCBM <
 
   // Patch staging is software-pipelined: the next tile's elements are loaded
   // into registers while this tile computes and stores.
-  const bf16* xb = reinterpret_cast<const bf16*>(a.x.ptr);
+  const H* xb = reinterpret_cast<const H*>(a.x.ptr);
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int t0 = L * a.tiles_per_blk, t1 = min(a.ntiles, t0 + a.tiles_per_blk);
-  bf16 pv[NPF];
+  H pv[NPF];
   unsigned pmask = 0;
   auto fetch = [&](int t) __attribute__((always_inline)) {
     const TileIdx ti = tile_at(t, a.tiles_w, a.tiles_h, a.y.d);
     const int d0 = ti.dz - a.pd, hb = ti.h0 - a.ph, wb = ti.w0 - a.pw;
-    const bf16* base = xb + corner(a.x, ti.nb, d0, hb, wb);
+    const H* base = xb + corner(a.x, ti.nb, d0, hb, wb);
     pmask = 0;
 #pragma unroll
     for (int k = 0; k < NPF; ++k) {
@@ -243,19 +243,19 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(KS * NCBM <
           v = (float)pv[k];
           if (a.prologue) v = pro_el(a.prologue, a.pro_scale, a.pro_shift, v, i / (a.kd * HH * WW));
         }
-        patch[i] = (bf16)v;
+        patch[i] = (H)v;
       }
     }
     __syncthreads();
     if (t + 1 < t1) fetch(t + 1);
-    bf16x8 bfr[2][KS];
+    typename V8<H>::type bfr[2][KS];
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr) {
       const int vo = (wave + 4 * rr) * WW + n;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) bfr[rr][s][j] = boff[s][j] >= 0 ? patch[boff[s][j] + vo] : (bf16)0.f;
+        for (int j = 0; j < 8; ++j) bfr[rr][s][j] = boff[s][j] >= 0 ? patch[boff[s][j] + vo] : (H)0.f;
     }
     const int64_t yc = corner(a.y, ti.nb, ti.dz, ti.h0, ti.w0);
     const int64_t rc = corner(a.res, ti.nb, ti.dz, ti.h0, ti.w0);
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(KS * NCBM <
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[i] = 0.f;
 #pragma unroll
-        for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[cb][s], bfr[rr][s], acc, 0, 0, 0);
+        for (int s = 0; s < KS; ++s) acc = mfma32x16(afr[cb][s], bfr[rr][s], acc);
         float* dst = lout + (vrow * 32 + n) * OROW + 4 * hf;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(KS * NCBM <
 // LDS and thread v sums its KK*KK shifted entries per output channel.  Stages
 // (tile, chunk) are software-pipelined through registers, and every
 // per-thread index is an offset from the stage's corner fixed for the launch.
-template <typename YT, int KK>
+template <typename YT, int KK, typename H>
 __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(3))) void conv_thin_out_kernel(ThinArgs a) {
   constexpr int HH = TH + KK - 1, WW = TWT + KK - 1;
   constexpr int U = HH * WW, UB = (U + 31) / 32;
@@ -326,7 +326,7 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(3))) void c
   const float aslope = a.act == VSRK_ACT_PRELU ? *a.act_param : 0.f;
   const float mslope = a.mask_slope ? *a.mask_slope : 0.f;
   const int mtap = n / a.cout, mco = n % a.cout;  // this lane's A row (tap, co)
-  const bf16* xb = reinterpret_cast<const bf16*>(a.x.ptr);
+  const H* xb = reinterpret_cast<const H*>(a.x.ptr);
   const int nch = ceil_div(a.cin, 32);
 
   // staging slots: chunk i = tid + k*THR is piece i&3 of halo voxel u = i>>2
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(3))) void c
   const int t0 = L * a.tiles_per_blk, t1 = min(a.ntiles, t0 + a.tiles_per_blk);
   const int s0 = t0 * nch, s1 = t1 * nch;
   uint4 rv[NLX];
-  bf16x8 afn[2], afr[2];  // A fragments (weights of the stage's chunk): next / current
+  typename V8<H>::type afn[2], afr[2];  // A fragments (weights of the stage's chunk): next / current
   unsigned rmask = 0;
   auto fetch = [&](int sg) __attribute__((always_inline)) {
     const TileIdx ti = tile_at(sg / nch, a.tiles_w, a.tiles_h, a.y.d);
@@ -355,11 +355,11 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(3))) void c
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int c = c0 + 16 * s + 8 * hf;
-      afn[s] = (n < M) ? *reinterpret_cast<const bf16x8*>(a.w + ((int64_t)mtap * a.cout_pad + mco) * a.cin_pad + c)
-                       : bf16x8{};
+      afn[s] = (n < M) ? *reinterpret_cast<const typename V8<H>::type*>(reinterpret_cast<const H*>(a.w) + ((int64_t)mtap * a.cout_pad + mco) * a.cin_pad + c)
+                       : typename V8<H>::type{};
     }
     const int hb = ti.h0 - a.ph, wb = ti.w0 - a.pw;
-    const bf16* base = xb + corner(a.x, ti.nb, ti.dz, hb, wb) + c0;
+    const H* base = xb + corner(a.x, ti.nb, ti.dz, hb, wb) + c0;
     rmask = 0;
 #pragma unroll
     for (int k = 0; k < NLX; ++k) {
@@ -390,10 +390,10 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(3))) void c
           if (a.prologue) {
             const int ch = q * 32 + 8 * (i & 3);
             float f[8];
-            Chunk<bf16>::unpack(v, f);
+            Chunk<H>::unpack(v, f);
 #pragma unroll
             for (int e = 0; e < 8; ++e) f[e] = pro_el(a.prologue, a.pro_scale, a.pro_shift, f[e], ch + e);
-            v = Chunk<bf16>::pack(f);
+            v = Chunk<H>::pack(f);
           }
         }
         *reinterpret_cast<uint4*>(xs + (i >> 2) * XROW + (i & 3) * 16) = v;
@@ -409,8 +409,8 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(3))) void c
       if (ub < UB) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(xs + (ub * 32 + n) * XROW + (16 * s + 8 * hf) * 2);
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[s], bfr, acc[i], 0, 0, 0);
+          const typename V8<H>::type bfr = *reinterpret_cast<const typename V8<H>::type*>(xs + (ub * 32 + n) * XROW + (16 * s + 8 * hf) * 2);
+          acc[i] = mfma32x16(afr[s], bfr, acc[i]);
         }
       }
     }
@@ -462,11 +462,11 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(3))) void c
 // by pad - (k-1)) gives the A operand A[(tap, co)][u] = dy[u - tap + pad][co].
 // Wave w runs k-steps w, w+4, w+8, w+12 (16 voxels each); the four wave
 // partials and the dbias partials are summed in a fixed order at the end.
-template <int NCI>
+template <int NCI, typename H>
 __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(NCI == 1 ? 3 : 2))) void conv_wgrad_thin_kernel(WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* xs = lds;                                           // [NCI][256][64 B]
-  bf16* dyp = reinterpret_cast<bf16*>(lds + NCI * 256 * 64);  // [cout][HH][WW]
+  H* dyp = reinterpret_cast<H*>(lds + NCI * 256 * 64);  // [cout][HH][WW]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, n = lane & 31, hf = lane >> 5;
   const int HH = GTH + a.kh - 1, WW = TW + a.kw - 1;
   const int taps2 = a.kh * a.kw, M = taps2 * a.cout;
@@ -481,8 +481,8 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(NCI == 1 ? 
   // transposed-read geometry (as conv_wgrad_kernel)
   const int g = lane >> 4, i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3;
   const int hfk = g >> 1, colb = ((g & 1) * 16 + 4 * pp) * 2;
-  const bf16* xb = reinterpret_cast<const bf16*>(a.x.ptr);
-  const bf16* yb = reinterpret_cast<const bf16*>(a.dy.ptr);
+  const H* xb = reinterpret_cast<const H*>(a.x.ptr);
+  const H* yb = reinterpret_cast<const H*>(a.dy.ptr);
 
   f32x16 acc[NCI];
 #pragma unroll
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(NCI == 1 ? 
   const int t_end = min(a.ntiles, t_begin + a.tiles_per_split);
   const int npat = a.cout * HH * WW;
   uint4 xr[4 * NCI];
-  bf16 yv[NPW];
+  H yv[NPW];
   unsigned xmask = 0, ymask = 0;
   auto fetch = [&](int t) __attribute__((always_inline)) {
     const TileIdx ti = tile_at(t, a.tiles_w, a.tiles_h, a.dy.d);
@@ -535,10 +535,10 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(NCI == 1 ? 
         if (a.prologue) {
           const int ch = ci0 + pl * 32 + 8 * p;
           float f[8];
-          Chunk<bf16>::unpack(val, f);
+          Chunk<H>::unpack(val, f);
 #pragma unroll
           for (int e = 0; e < 8; ++e) f[e] = pro_el(a.prologue, a.pro_scale, a.pro_shift, f[e], ch + e);
-          val = Chunk<bf16>::pack(f);
+          val = Chunk<H>::pack(f);
         }
       }
       *reinterpret_cast<uint4*>(xs + (pl * 256 + v) * 64 + p * 16) = val;
@@ -546,7 +546,7 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(NCI == 1 ? 
 #pragma unroll
     for (int k = 0; k < NPW; ++k) {
       const int i = tid + k * THR;
-      if (i < npat) dyp[i] = ((ymask >> k) & 1) ? yv[k] : (bf16)0.f;
+      if (i < npat) dyp[i] = ((ymask >> k) & 1) ? yv[k] : (H)0.f;
     }
     __syncthreads();
     if (t + 1 < t_end) fetch(t + 1);
@@ -554,20 +554,20 @@ __global__ __launch_bounds__(THR) __attribute__((amdgpu_waves_per_eu(NCI == 1 ? 
     for (int i = 0; i < 4; ++i) {
       const int vb = (wave + 4 * i) * 16;
       const int vrow = vb / TW, vc0 = vb % TW;
-      bf16x8 af;
+      typename V8<H>::type af;
       if (n < M) {
         const int base = (mco * HH + vrow - mkh + a.kh - 1) * WW + vc0 + 8 * hf - mkw + a.kw - 1;
 #pragma unroll
         for (int j = 0; j < 8; ++j) af[j] = dyp[base + j];
       } else {
-        af = bf16x8{};
+        af = typename V8<H>::type{};
       }
 #pragma unroll
       for (int p = 0; p < NCI; ++p) {
         const char* px = xs + (p * 256 + vrow * TW + vc0 + 8 * hfk + qq) * 64 + colb;
         const v4i16 x0 = ds_read_tr(px), x1 = ds_read_tr(px + 4 * 64);
-        const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
-        acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[p], 0, 0, 0);
+        const typename V8<H>::type bfr = __builtin_bit_cast(typename V8<H>::type, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+        acc[p] = mfma32x16(af, bfr, acc[p]);
       }
     }
     if (do_bias) {
@@ -657,7 +657,7 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                        const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s) {
   if (!thin_enabled()) return 0;
-  if (x->dtype != VSRK_BF16) return 0;
+  if (!vsrk_is16(x->dtype)) return 0;
   if (x->shuffle > 1 || y->shuffle > 1 || d->bias_perm_r > 1) return 0;
   if ((residual && residual->shuffle > 1) || (mask && mask->shuffle > 1)) return 0;
   const int K = d->kd * d->kh * d->kw * x->c;
@@ -672,7 +672,7 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   a.y = make_view(y);
   a.res = residual ? make_view(residual) : a.y;
   a.msk = mask ? make_view(mask) : a.y;
-  a.w = (const bf16*)w_packed;
+  a.w = w_packed;
   a.bias = bias;
   a.pro_scale = pro_scale;
   a.pro_shift = pro_shift;
@@ -689,7 +689,7 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   a.accumulate = d->accumulate;
   a.has_res = residual != nullptr;
   a.has_mask = mask != nullptr;
-  const int yes = y->dtype == VSRK_BF16 ? 2 : 4;
+  const int yes = vsrk_esize(y->dtype);
   a.vec = chunk_ok(y, yes) && (!residual || chunk_ok(residual, yes)) && (!mask || chunk_ok(mask, yes));
   a.out_scale = d->out_scale;
   a.tiles_h = ceil_div(y->h, TH);
@@ -701,14 +701,18 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   }
   a.ntiles = (int)ntiles;
   if (a.ntiles == 0) return 1;
-  const bool yb = y->dtype == VSRK_BF16;
+  const bool yb = y->dtype != VSRK_F32;  // 16-bit output (the input's type)
   if (thin_in) {
     const size_t lds = (size_t)256 * OROW * 4 + PATCH_MAX * 2;  // 36.9 KB + 2 KB: 3 workgroups per CU
     const int ncb = ceil_div(y->c, 32);
 #define VSRK_THIN_IN(KS, NCB)                                                     \
   do {                                                                            \
-    if (yb) launch_persistent(conv_thin_in_kernel<bf16, KS, NCB>, a, lds, s);     \
-    else launch_persistent(conv_thin_in_kernel<float, KS, NCB>, a, lds, s);       \
+    vsrk_dispatch16(x->dtype, [&](auto tag) {                                     \
+      using H = decltype(tag);                                                    \
+      if (yb) launch_persistent(conv_thin_in_kernel<H, KS, NCB, H>, a, lds, s);   \
+      else launch_persistent(conv_thin_in_kernel<float, KS, NCB, H>, a, lds, s);  \
+      return 0;                                                                   \
+    });                                                                           \
   } while (0)
     if (K <= 16) {
       if (ncb <= 2) VSRK_THIN_IN(1, 2);
@@ -722,13 +726,17 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
 #undef VSRK_THIN_IN
   } else {
     const size_t lds = (size_t)UMAX * XROW + (size_t)d->kh * d->kw * y->c * UMAX * 4;
-    if (d->kh == 3) {
-      if (yb) launch_persistent(conv_thin_out_kernel<bf16, 3>, a, lds, s);
-      else launch_persistent(conv_thin_out_kernel<float, 3>, a, lds, s);
-    } else {
-      if (yb) launch_persistent(conv_thin_out_kernel<bf16, 1>, a, lds, s);
-      else launch_persistent(conv_thin_out_kernel<float, 1>, a, lds, s);
-    }
+    vsrk_dispatch16(x->dtype, [&](auto tag) {
+      using H = decltype(tag);
+      if (d->kh == 3) {
+        if (yb) launch_persistent(conv_thin_out_kernel<H, 3, H>, a, lds, s);
+        else launch_persistent(conv_thin_out_kernel<float, 3, H>, a, lds, s);
+      } else {
+        if (yb) launch_persistent(conv_thin_out_kernel<H, 1, H>, a, lds, s);
+        else launch_persistent(conv_thin_out_kernel<float, 1, H>, a, lds, s);
+      }
+      return 0;
+    });
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -740,7 +748,7 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
 
 // Weight gradient of a conv with cout <= 3 (the tail conv F -> 1): same plan
 // (splits x combos, slab size) as vsrk_conv_wgrad, so the reduce is shared.
-int vsrk_conv_wgrad_thin(const vsrk_conv::WgradArgs& a, int nco, int nci, int perm_r, hipStream_t s) {
+int vsrk_conv_wgrad_thin(const vsrk_conv::WgradArgs& a, int nco, int nci, int perm_r, int dtype, hipStream_t s) {
   if (!thin_enabled()) return 0;
   if (nco != 1 || a.cout > 3 || a.kd != 1 || a.pd != 0 || a.kh != a.kw || a.kh * a.kw * a.cout > 32) return 0;
   if (a.cin % 8 || !a.xvec || a.x.r > 1 || a.dy.r > 1 || perm_r > 1) return 0;
@@ -748,14 +756,12 @@ int vsrk_conv_wgrad_thin(const vsrk_conv::WgradArgs& a, int nco, int nci, int pe
   if (a.cout * (GTH + a.kh - 1) * (TW + a.kw - 1) > NPW * THR) return 0;
   const size_t stage = (size_t)nci * 256 * 64 + (size_t)a.cout * (GTH + a.kh - 1) * (TW + a.kw - 1) * 2;
   const size_t lds = std::max(stage, (size_t)4 * nci * 1024 * 4);
-  if (nci == 2) {
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_thin_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    conv_wgrad_thin_kernel<2><<<a.nblk, THR, lds, s>>>(a);
-  } else {
-    (void)hipFuncSetAttribute((const void*)conv_wgrad_thin_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    conv_wgrad_thin_kernel<1><<<a.nblk, THR, lds, s>>>(a);
-  }
+  vsrk_dispatch16(dtype, [&](auto tag) {
+    using H = decltype(tag);
+    auto kern = nci == 2 ? conv_wgrad_thin_kernel<2, H> : conv_wgrad_thin_kernel<1, H>;
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    kern<<<a.nblk, THR, lds, s>>>(a);
+    return 0;
+  });
   return 1;
 }

@@ -451,7 +451,7 @@ extern "C" int vsrk_conv_wgrad(const vsrk_conv_desc* d, const vsrk_tensor5* x, c
   a.cin_pad = round_up(x->c, 32 * p.nci);
   if (p.ntiles == 0) return VSRK_OK;
   const bool vec = a.xvec && a.dyvec;
-  if (x->dtype == VSRK_BF16 && vsrk_conv_wgrad_thin(a, p.nco, p.nci, perm_r, s)) {
+  if (vsrk_is16(x->dtype) && vsrk_conv_wgrad_thin(a, p.nco, p.nci, perm_r, x->dtype, s)) {
     // thin-channel kernel (conv_thin.hip), same slab layout
   } else if (x->dtype == VSRK_BF16 && vec && vsrk_conv_wgrad_fast(a, p.nco, p.nci, s)) {
     // LDS-DMA kernel (conv_wgrad_fast.hip), same slab layout
