@@ -225,6 +225,15 @@ int vsrk_ssim(const float* out, const float* target, int32_t batch, int32_t chan
               int32_t denormalize, float mean, float std, float value_range, float* ssim_per_sample, float* ssim_mean,
               void* workspace, size_t workspace_bytes, void* stream);
 
+/* SSIM(dim=3) of (N, C, D, H, W) fp32 volumes: the same Gaussian window
+ * (metrics.py:66-79) as an 11x11x11 product, valid filtering; depth pass to
+ * five moment volumes, then the separable in-plane pass.  Replaces
+ * SSIM(dim=3).forward (metrics.py:86-113). */
+size_t vsrk_ssim3d_workspace_size(int32_t batch, int32_t channels, int32_t d, int32_t h, int32_t w);
+int vsrk_ssim3d(const float* out, const float* target, int32_t batch, int32_t channels, int32_t d, int32_t h,
+                int32_t w, int32_t denormalize, float mean, float std, float value_range, float* ssim_per_sample,
+                float* ssim_mean, void* workspace, size_t workspace_bytes, void* stream);
+
 /* BatchNorm3d, training statistics (duf_net.py:116,198,201,209,212).  Split
  * so a data-parallel caller can all-reduce the per-channel sums between the
  * calls (SyncBatchNorm):

@@ -388,6 +388,42 @@ def run_metrics():
         fx[f"ssim_{ds}"] = float(metrics.SSIM()(od, td))
     torch.save(fx, OUT / "metrics.pt")
     print(f"metrics: psnr_acdc={fx['psnr_acdc']:.4f} ssim_acdc={fx['ssim_acdc']:.4f}")
+    run_metrics3d(metrics, utils)
+
+
+def run_metrics3d(metrics, utils):
+    """SSIM(dim=3) on denormalized volumes and the Cardiac bounding-box
+    variants (metrics.py:39-165), evaluated by the reference itself.  The
+    coordinates file the Cardiac metrics read is a pickle the reference's
+    own preprocessing writes (metrics.py:123-125); here it is written by this
+    script from a plain dict, and the fixture keeps the dict."""
+    import pickle
+    import tempfile
+    g = torch.Generator().manual_seed(8)
+    o = torch.randn((2, 1, 14, 20, 24), generator=g)
+    t = o * 0.7 + 0.3 * torch.randn((2, 1, 14, 20, 24), generator=g)
+    od, td = utils.denormalize(o, "acdc"), utils.denormalize(t, "acdc")
+    ssim3 = metrics.SSIM(dim=3)
+    mine = cpu_nets.ssim(od, td, dim=3)
+    assert torch.allclose(ssim3(od, td), mine, rtol=1e-6, atol=1e-7)
+    fx = {"out": o, "target": t, "ssim3d_acdc": float(ssim3(od, td)),
+          "ssim3d_acdc_per_sample": metrics.SSIM(dim=3, size_average=False)(od, td)}
+    # Cardiac crops on 2-D slices (the validation path crops (..., h0:hn, w0:wn))
+    o2, t2 = od[:, :, 3], td[:, :, 3]  # (N, 1, 20, 24)
+    coords = {"patient001": (2, 17, 3, 20), "patient042": (0, 20, 5, 24)}
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "coords.pkl")
+        with open(path, "wb") as fh:
+            pickle.dump(coords, fh)
+        fx["cardiac"] = {}
+        for name in coords:
+            cp = metrics.CardiacPSNR(path)(o2, t2, name)
+            cs = metrics.CardiacSSIM(path)(o2, t2, name)
+            fx["cardiac"][name] = {"psnr": float(cp), "ssim": float(cs)}
+    fx["cardiac_coords"] = coords
+    fx["cardiac_out"], fx["cardiac_target"] = o2, t2
+    torch.save(fx, OUT / "metrics3d.pt")
+    print(f"metrics3d: ssim3d_acdc={fx['ssim3d_acdc']:.6f} cardiac={fx['cardiac']}")
 
 
 def main():
@@ -395,6 +431,9 @@ def main():
         raise SystemExit("reference not available (build container only)")
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     only = os.environ.get("GOLDEN_ONLY")
+    if only == "metrics":
+        run_metrics()
+        return
     for name, spec in CASES.items():
         if only and name not in only.split(","):
             continue

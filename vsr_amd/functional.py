@@ -263,11 +263,24 @@ def psnr(out: torch.Tensor, target: torch.Tensor, mean: float = 0.0, std: float 
 
 def ssim(out: torch.Tensor, target: torch.Tensor, mean: float = 0.0, std: float = 1.0, value_range: float = 255.0,
          denormalize: bool = False):
-    """2-D SSIM of (N, C, H, W) images ([denormalized] in the kernel); returns
-    (batch mean, per-sample) as device tensors."""
+    """SSIM of (N, C, H, W) images (2-D window) or (N, C, D, H, W) volumes
+    (3-D window) ([denormalized] in the kernel); returns (batch mean,
+    per-sample) as device tensors."""
     lib = _lib()
+    if out.dim() == 5:
+        o = out.float().contiguous()
+        t = target.float().contiguous()
+        b, c, d, h, w = o.shape
+        ps = torch.empty(b, dtype=torch.float32, device=o.device)
+        m = torch.empty((), dtype=torch.float32, device=o.device)
+        nb = lib.vsrk_ssim3d_workspace_size(b, c, d, h, w)
+        ws = torch.empty(nb, dtype=torch.uint8, device=o.device)
+        N.check(lib.vsrk_ssim3d(o.data_ptr(), t.data_ptr(), b, c, d, h, w, 1 if denormalize else 0, float(mean),
+                                float(std), float(value_range), ps.data_ptr(), m.data_ptr(), ws.data_ptr(), nb,
+                                N.stream_ptr(o.device)), "ssim3d")
+        return m, ps
     if out.dim() != 4:
-        raise ValueError(f"ssim: expected (N, C, H, W) images, got {tuple(out.shape)}")
+        raise ValueError(f"ssim: expected (N, C, H, W) images or (N, C, D, H, W) volumes, got {tuple(out.shape)}")
     o = out.float().contiguous()
     t = target.float().contiguous()
     b, c, h, w = o.shape

@@ -5,7 +5,7 @@ kernel plus a fixed-order final reduction; ``psnr_denorm`` / ``ssim_denorm``
 fuse the trainer's denormalize (utils.py:1-20) into them, which is what the
 train step calls every iteration (base_trainer.py:135).  CardiacPSNR /
 CardiacSSIM (metrics.py:116-165) crop the cardiac bounding box (a view) and
-reuse them.
+reuse them.  SSIM(dim=3) filters depth first (vsrk_ssim3d).
 """
 from __future__ import annotations
 
@@ -45,14 +45,12 @@ def ssim_denorm(output: torch.Tensor, target: torch.Tensor, dataset: str, size_a
 
 
 class SSIM(nn.Module):
-    """metrics.py:39-113 (dim=2): Gaussian 11x11 window (sigma 1.5), valid filtering."""
+    """metrics.py:39-113: Gaussian 11^dim window (sigma 1.5), valid filtering; dim 2 or 3."""
 
     def __init__(self, dim=2, channels=1, size_average=True, value_range=255):
         super().__init__()
         if dim not in (2, 3):
             raise ValueError(f"Only dim=2, 3 are supported. Received dim={dim}.")
-        if dim == 3:
-            raise NotImplementedError("the HIP SSIM covers dim=2 (what every reference config uses)")
         self.dim = dim
         self.channels = channels
         self.size_average = size_average
@@ -61,16 +59,34 @@ class SSIM(nn.Module):
         self.c2 = (0.03 * value_range) ** 2
 
     def forward(self, output, target):
+        if output.dim() != self.dim + 2:
+            raise ValueError(f"SSIM(dim={self.dim}) expects (N, C, *) with {self.dim} spatial dims, "
+                             f"got {tuple(output.shape)}")
         m, per = F.ssim(output, target, value_range=self.value_range)
         return m if self.size_average else per
 
 
 def _load_coordinates(path):
-    """The reference pickles {patient name: (h0, hn, w0, wn)} (metrics.py:123-125).
-    Only a JSON map is read here (no unpickling of input files)."""
+    """{patient name: (h0, hn, w0, wn)}.  The reference reads a pickle
+    (metrics.py:123-125) written by its preprocessing; that format is read here
+    with an unpickler that resolves no globals (only dict / tuple / list / str
+    / int / float containers can be built, nothing in the file is executed).
+    A JSON map {name: [h0, hn, w0, wn]} is accepted too."""
     import json
-    with open(path) as fh:
-        return {k: tuple(v) for k, v in json.load(fh).items()}
+    import pickle
+
+    class _DataOnly(pickle.Unpickler):
+        def find_class(self, module, name):
+            raise pickle.UnpicklingError(f"coordinates file references {module}.{name}: only plain data is read")
+
+    with open(path, "rb") as fh:
+        head = fh.read(1)
+        fh.seek(0)
+        if head in (b"{", b" ", b"\n"):
+            data = json.loads(fh.read().decode())
+        else:
+            data = _DataOnly(fh).load()
+    return {str(k): tuple(int(x) for x in v) for k, v in data.items()}
 
 
 class CardiacPSNR(nn.Module):
