@@ -288,6 +288,13 @@ int vsrk_duf_dynfilter_bwd(const float* x, const float* logits, const float* gra
 const char* vsrk_last_error(void);
 const char* vsrk_version(void);
 
+/* LR synthesis (acdc_preprocess.py:102-180, Downscale): cv2.resize with
+ * INTER_CUBIC of n fp64 images (ih, iw) -> (oh, ow) (source coordinate
+ * (d + 0.5) * ih / oh - 0.5, Keys cubic A = -0.75, border indices clamped),
+ * then, with round_clip, np.clip(round(.), 0, 255). */
+int vsrk_resize_bicubic(const double* src, int32_t n, int32_t ih, int32_t iw, int32_t oh, int32_t ow, double* dst,
+                        int32_t round_clip, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -90,6 +90,7 @@ _SIGS = {
     "vsrk_ssim_workspace_size": (C.c_size_t, [C.c_int32] * 4),
     "vsrk_ssim": (C.c_int, [_P, _P] + [C.c_int32] * 5 + [C.c_float] * 3 + [_P, _P, _P, C.c_size_t, _P]),
     "vsrk_ssim3d_workspace_size": (C.c_size_t, [C.c_int32] * 5),
+    "vsrk_resize_bicubic": (C.c_int, [_P] + [C.c_int32] * 5 + [_P, C.c_int32, _P]),
     "vsrk_ssim3d": (C.c_int, [_P, _P] + [C.c_int32] * 6 + [C.c_float] * 3 + [_P, _P, _P, C.c_size_t, _P]),
     "vsrk_last_error": (C.c_char_p, []),
     "vsrk_version": (C.c_char_p, []),

@@ -409,3 +409,63 @@ extern "C" int vsrk_psnr(const float* out, const float* target, int32_t batch, i
   VSRK_LAUNCH_CHECK("psnr_final");
   return VSRK_OK;
 }
+
+// ---------------------------------------------------------------------------
+// LR synthesis (acdc_preprocess.py:102-180, Downscale): the bicubic resize of
+// the k-space-truncated image, cv2.resize(INTER_CUBIC) on float64 input as
+// OpenCV computes it: the source coordinate fx = float((d + 0.5) * s - 0.5),
+// the Keys cubic (A = -0.75) weights of its fraction in float, indices clamped
+// at the borders, a horizontal pass per source row then the vertical pass,
+// each as a left-to-right sum of double products (no contraction) -- then
+// np.clip(img.round(), 0, 255).  One thread per output pixel (offline data
+// preparation, tiny next to the step).
+namespace {
+__device__ __forceinline__ void cubic_w(float x, float* w) {
+#pragma clang fp contract(off)
+  const float A = -0.75f;
+  w[0] = ((A * (x + 1) - 5 * A) * (x + 1) + 8 * A) * (x + 1) - 4 * A;
+  w[1] = ((A + 2) * x - (A + 3)) * x * x + 1;
+  w[2] = ((A + 2) * (1 - x) - (A + 3)) * (1 - x) * (1 - x) + 1;
+  w[3] = 1.f - w[0] - w[1] - w[2];
+}
+__global__ void resize_bicubic_kernel(const double* __restrict__ src, int n, int ih, int iw, int oh, int ow,
+                                      double* __restrict__ dst, int round_clip) {
+#pragma clang fp contract(off)
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)n * oh * ow) return;
+  const int x = (int)(i % ow);
+  const int64_t t = i / ow;
+  const int y = (int)(t % oh);
+  const int b = (int)(t / oh);
+  const double scy = 1.0 / ((double)oh / ih), scx = 1.0 / ((double)ow / iw);
+  float fy = (float)((y + 0.5) * scy - 0.5), fx = (float)((x + 0.5) * scx - 0.5);
+  const int y0 = (int)floorf(fy), x0 = (int)floorf(fx);
+  fy -= y0;
+  fx -= x0;
+  float wy[4], wx[4];
+  cubic_w(fy, wy);
+  cubic_w(fx, wx);
+  const double* im = src + (int64_t)b * ih * iw;
+  double rows[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const double* r = im + (int64_t)min(max(y0 - 1 + a, 0), ih - 1) * iw;
+    const double s0 = r[min(max(x0 - 1, 0), iw - 1)], s1 = r[min(max(x0, 0), iw - 1)];
+    const double s2 = r[min(max(x0 + 1, 0), iw - 1)], s3 = r[min(max(x0 + 2, 0), iw - 1)];
+    rows[a] = s0 * (double)wx[0] + s1 * (double)wx[1] + s2 * (double)wx[2] + s3 * (double)wx[3];
+  }
+  double acc = rows[0] * (double)wy[0] + rows[1] * (double)wy[1] + rows[2] * (double)wy[2] + rows[3] * (double)wy[3];
+  if (round_clip) acc = fmin(fmax(rint(acc), 0.0), 255.0);
+  dst[i] = acc;
+}
+}  // namespace
+
+extern "C" int vsrk_resize_bicubic(const double* src, int32_t n, int32_t ih, int32_t iw, int32_t oh, int32_t ow,
+                                   double* dst, int32_t round_clip, void* stream) {
+  VSRK_CHECK(src && dst && n > 0 && ih > 0 && iw > 0 && oh > 0 && ow > 0, "resize_bicubic: bad argument");
+  const int64_t total = (int64_t)n * oh * ow;
+  resize_bicubic_kernel<<<(int)ceil_div64(total, 256), 256, 0, (hipStream_t)stream>>>(src, n, ih, iw, oh, ow, dst,
+                                                                                      round_clip);
+  VSRK_LAUNCH_CHECK("resize_bicubic");
+  return VSRK_OK;
+}

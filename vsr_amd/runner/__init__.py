@@ -1,2 +1,2 @@
-"""Train loop mirror of src/runner (trainers resolvable by name, main.py:99)."""
-from . import trainers  # noqa: F401
+"""Train / test loop mirror of src/runner (trainers and predictors resolvable by name, main.py:99,113)."""
+from . import predictors, trainers  # noqa: F401

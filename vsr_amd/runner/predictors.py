@@ -1,0 +1,232 @@
+"""Test-time loop mirror of src/runner/predictors (resolved by name, main.py:110-156).
+
+BasePredictor (base_predictor.py:6-136) and the ACDC / DSB15 SISR, MISR and
+VSR predictors (acdc_{sisr,misr,vsr}_predictor.py, dsb15_*): batch size 1,
+the network in eval mode, per-frame losses and metrics on the HIP kernels
+(PSNR / SSIM fused with denormalize, Cardiac* by patient name), the same
+log keys, and -- with ``exported=True`` -- the results CSV (one row per
+frame: name, metrics, losses), a PNG per SR frame and a GIF per sequence.
+
+Differences: images are written with PIL (the reference's scipy.misc.imsave
+was removed from SciPy and imageio is not a dependency here); checkpoints
+load with ``weights_only=True``.
+"""
+from __future__ import annotations
+
+import csv
+import logging
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from .. import metrics as M
+from ..utils import denormalize
+from .trainers import _metric
+
+
+class BasePredictor:
+    """base_predictor.py:6-136."""
+
+    dataset_name = "acdc"
+
+    def __init__(self, device, test_dataloader, net, loss_fns, loss_weights, metric_fns, saved_dir=None,
+                 exported=False):
+        self.device = device
+        self.test_dataloader = test_dataloader
+        self.net = net.to(device)
+        self.loss_fns = [fn.to(device) for fn in loss_fns]
+        self.loss_weights = torch.tensor(loss_weights, dtype=torch.float, device=device)
+        self.metric_fns = [fn.to(device) for fn in metric_fns]
+        if getattr(test_dataloader, "batch_size", 1) != 1:
+            raise ValueError(f"The testing batch size should be 1. Got {test_dataloader.batch_size}.")
+        self.exported = exported
+        self.saved_dir = Path(saved_dir) if exported else None
+
+    # -- reference hooks ------------------------------------------------------
+    def _allocate_data(self, batch):
+        if isinstance(batch, dict):
+            return {k: self._allocate_data(v) for k, v in batch.items()}
+        if isinstance(batch, list):
+            return [self._allocate_data(v) for v in batch]
+        if isinstance(batch, tuple):
+            return tuple(self._allocate_data(v) for v in batch)
+        if isinstance(batch, torch.Tensor):
+            return batch.to(self.device)
+        return batch
+
+    def _init_log(self):
+        log = {"Loss": 0.0}
+        for fn in self.loss_fns:
+            log[fn.__class__.__name__] = 0.0
+        for fn in self.metric_fns:
+            log[fn.__class__.__name__] = 0.0
+        return log
+
+    def load(self, path):
+        """base_predictor.py:130-136 (net state only), without unpickling code."""
+        ckpt = torch.load(path, map_location=self.device, weights_only=True)
+        self.net.load_state_dict(ckpt["net"])
+
+    # -- per-frame pieces (shared by the SISR / MISR / VSR predictors) ----------
+    def _frame_losses(self, outputs, targets):
+        """(T, #loss_fns) -- acdc_vsr_predictor.py:118-130."""
+        return torch.stack([torch.stack([fn(o, t) for o, t in zip(outputs, targets)]) for fn in self.loss_fns],
+                           dim=1)
+
+    def _frame_metrics(self, outputs, targets, name):
+        """(T, #metric_fns) on denormalized frames -- acdc_vsr_predictor.py:132-151."""
+        rows = []
+        for fn in self.metric_fns:
+            vals = []
+            for o, t in zip(outputs, targets):
+                if "Cardiac" in fn.__class__.__name__:
+                    vals.append(fn(denormalize(o, self.dataset_name), denormalize(t, self.dataset_name), name))
+                else:
+                    vals.append(_metric(fn, o, t, self.dataset_name))
+            rows.append(torch.stack([v.reshape(()) for v in vals]))
+        return torch.stack(rows, dim=1)
+
+    def _sample_name(self, index):
+        """Patient and sequence id from the dataset's file names (acdc_vsr_predictor.py:55-58)."""
+        data = getattr(self.test_dataloader.dataset, "data", None)
+        if data is None:
+            return f"sample{int(index)}", "patient", f"sequence{int(index)}"
+        lr_path = Path(data[int(index)][0])
+        filename = lr_path.parts[-1].split(".")[0]
+        parts = filename.split("_")
+        patient, sid = parts[0], parts[-1]
+        return filename, patient, sid
+
+    def _to_uint8(self, x):
+        return denormalize(x, self.dataset_name).squeeze().detach().cpu().numpy().astype(np.uint8)
+
+    @staticmethod
+    def _save_png(path, img):
+        from PIL import Image
+        Image.fromarray(img).save(path)
+
+    @staticmethod
+    def _dump_video(path, imgs):
+        """acdc_vsr_predictor.py:172-180: the SR frames as one GIF."""
+        from PIL import Image
+        frames = [Image.fromarray(i) for i in imgs]
+        frames[0].save(path, save_all=True, append_images=frames[1:], loop=0)
+
+    # -- the loop ---------------------------------------------------------------
+    def _get_inputs_targets(self, batch):
+        raise NotImplementedError
+
+    def _frames_of(self, outputs, targets):
+        """Per-frame lists (T entries)."""
+        raise NotImplementedError
+
+    def predict(self):
+        self.net.eval()
+        header = (["name"] + [fn.__class__.__name__ for fn in self.metric_fns] +
+                  [fn.__class__.__name__ for fn in self.loss_fns])
+        results = [header]
+        log = self._init_log()
+        count = 0
+        for batch in self.test_dataloader:
+            batch = self._allocate_data(batch)
+            inputs, targets, index = self._get_inputs_targets(batch)
+            with torch.no_grad():
+                filename, patient, sid = self._sample_name(index)
+                outputs = self.net(inputs)
+                outs, tgts = self._frames_of(outputs, targets)
+                losses = self._frame_losses(outs, tgts)                  # (T, L)
+                loss = (losses.mean(dim=0) * self.loss_weights).sum()
+                metrics = self._frame_metrics(outs, tgts, patient)      # (T, M)
+            T = len(outs)
+            if self.exported:
+                rows = torch.cat([metrics, losses], dim=1).cpu().tolist()
+                stem = filename.replace("2d+1d", "2d").replace("sequence", "slice")
+                for t, row in enumerate(rows):
+                    results.append([stem + f"_frame{t + 1:0>2d}", *row])
+                imgs = [self._to_uint8(o) for o in outs]
+                vdir = self.saved_dir / "videos" / patient
+                idir = self.saved_dir / "imgs" / patient
+                vdir.mkdir(parents=True, exist_ok=True)
+                idir.mkdir(parents=True, exist_ok=True)
+                self._dump_video(vdir / f"{sid}.gif", imgs)
+                for t, img in enumerate(imgs):
+                    self._save_png(idir / (sid.replace("sequence", "slice") + f"_frame{t + 1:0>2d}.png"), img)
+            # acdc_vsr_predictor.py:160-170: frame-weighted
+            log["Loss"] += loss.item() * T
+            for fn, v in zip(self.loss_fns, losses.mean(dim=0)):
+                log[fn.__class__.__name__] += v.item() * T
+            for fn, v in zip(self.metric_fns, metrics.mean(dim=0)):
+                log[fn.__class__.__name__] += v.item() * T
+            count += T
+        if self.exported:
+            self.saved_dir.mkdir(parents=True, exist_ok=True)
+            with open(self.saved_dir / "results.csv", "w", newline="") as fh:
+                csv.writer(fh).writerows(results)
+        for k in log:
+            log[k] /= max(count, 1)
+        logging.info(f"Test log: {log}.")
+        return log
+
+
+class AcdcVSRPredictor(BasePredictor):
+    """acdc_vsr_predictor.py:15-180: list of T LR frames -> T SR frames."""
+
+    def _get_inputs_targets(self, batch):
+        return batch["lr_imgs"], batch["hr_imgs"], batch["index"]
+
+    def _frames_of(self, outputs, targets):
+        return list(outputs), list(targets)
+
+
+class Dsb15VSRPredictor(AcdcVSRPredictor):
+    dataset_name = "dsb15"
+
+
+class AcdcMISRPredictor(BasePredictor):
+    """acdc_misr_predictor.py: T LR frames -> the centre SR frame."""
+
+    def _get_inputs_targets(self, batch):
+        return batch["lr_imgs"], batch["hr_img"], batch["index"]
+
+    def _frames_of(self, output, target):
+        return [output], [target]
+
+
+class Dsb15MISRPredictor(AcdcMISRPredictor):
+    dataset_name = "dsb15"
+
+
+class AcdcSISRPredictor(BasePredictor):
+    """acdc_sisr_predictor.py: one LR slice -> one SR slice."""
+
+    def _get_inputs_targets(self, batch):
+        return batch["lr_img"], batch["hr_img"], batch["index"]
+
+    def _frames_of(self, output, target):
+        return [output], [target]
+
+
+class Dsb15SISRPredictor(AcdcSISRPredictor):
+    dataset_name = "dsb15"
+
+
+class AcdcSISRSRFBPredictor(AcdcSISRPredictor):
+    """acdc_sisr_srfb_predictor.py: feedback nets return every step; losses
+    are averaged over the steps (:94-108), metrics score the last (:110-128)."""
+
+    def _frames_of(self, outputs, target):
+        self._steps = (list(outputs), target)
+        return [outputs[-1]], [target]
+
+    def _frame_losses(self, outs, tgts):
+        steps, target = self._steps
+        return torch.stack([torch.stack([fn(o, target) for o in steps]).mean() for fn in self.loss_fns]).view(1, -1)
+
+
+class Dsb15SISRSRFBPredictor(AcdcSISRSRFBPredictor):
+    dataset_name = "dsb15"
+
+
+__all__ = ["BasePredictor", "AcdcVSRPredictor", "Dsb15VSRPredictor", "AcdcMISRPredictor", "Dsb15MISRPredictor",
+           "AcdcSISRPredictor", "Dsb15SISRPredictor", "AcdcSISRSRFBPredictor", "Dsb15SISRSRFBPredictor", "M"]
