@@ -198,3 +198,58 @@ def test_multitile_wgrad(case, dtype):
         ew = (res[0][0].double() - wr.grad).abs().max().item()
         eb = (res[0][1].double() - br.grad).abs().max().item()
         assert ew <= tw and eb <= tb, (name, cap, ew, tw, eb, tb)
+
+
+PIPE = [
+    ("duf_3d_bn", 2, 5, 20, 40, 64, 32, (3, 3, 3), (1, 1, 1), True, True),
+    ("duf_3d_valid", 2, 5, 20, 40, 96, 32, (3, 3, 3), (0, 1, 1), True, True),
+    ("edsr_64", 3, 1, 40, 70, 64, 64, (1, 3, 3), (0, 1, 1), False, True),
+    ("ragged_ch", 2, 3, 13, 37, 40, 24, (3, 3, 3), (1, 1, 1), True, False),
+    ("wide_in", 2, 4, 12, 50, 224, 32, (3, 3, 3), (0, 1, 1), True, True),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", PIPE, ids=[c[0] for c in PIPE])
+def test_wgrad_pipe_matches_generic(case, dtype):
+    """The two-stage pipelined 3x3(x3) weight gradient (conv_wgrad_pipe.hip)
+    runs the generic kernel's MFMA sequence on the same staged operands, so
+    dW and dbias are bitwise equal to it, for every grid cap (several tiles
+    per workgroup drive the ring), and within bf16/fp16 tolerance of fp64."""
+    name, n, d, h, w, ci, co, k, pad, bn, bias = case
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn((n, d, h, w, ci), generator=g)
+    do = d + 2 * pad[0] - k[0] + 1
+    gy = torch.randn((n, do, h, w, co), generator=g)
+    sc = torch.rand(ci, generator=g) + 0.5
+    sh = torch.randn(ci, generator=g)
+    kw = dict(prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV)) if bn else {}
+    xd, gd = x.to(DEV, dtype), gy.to(DEV, dtype)
+
+    def run(pipe, cap):
+        F.set_conv_path("wgrad_pipe", pipe)
+        F.set_grid_cap(cap)
+        try:
+            dw = torch.empty((co, ci, *k), dtype=torch.float32, device=DEV)
+            db = torch.empty(co, dtype=torch.float32, device=DEV) if bias else None
+            F.conv_wgrad(xd, gd, k, pad, dw, db, **kw)
+            return dw.cpu(), (db.cpu() if bias else None)
+        finally:
+            F.set_conv_path("wgrad_pipe", -1)
+            F.set_grid_cap(0)
+
+    xin = _q(x, dtype)
+    if bn:
+        xin = torch.relu(xin * sc.double() + sh.double()).to(dtype).double()
+    wr = torch.zeros((co, ci, *k), dtype=torch.float64, requires_grad=True)
+    br = torch.zeros(co, dtype=torch.float64, requires_grad=True)
+    _ref_conv(xin, wr, br, pad).backward(_q(gy, dtype))
+    for cap in (0, 3):
+        pw, pb = run(1, cap)
+        gw, gb = run(0, cap)
+        assert torch.equal(pw, gw), (name, cap, (pw - gw).abs().max().item())
+        if bias:
+            assert torch.equal(pb, gb), (name, cap)
+        assert (pw.double() - wr.grad).abs().max().item() <= 1e-2 * (1 + wr.grad.abs().max().item())
+        if bias:
+            assert (pb.double() - br.grad).abs().max().item() <= 1e-2 * (1 + br.grad.abs().max().item())

@@ -65,6 +65,7 @@ def main():
     nbytes = {"fwd": x.numel() // x.shape[-1] * (ci * 2) + y.numel() * esz[y.dtype],
               "dgrad": gy.numel() // gy.shape[-1] * (co * 2) + dx.numel() * esz[dx.dtype],
               "fwdpro": x.numel() // x.shape[-1] * (ci * 2) + y.numel() * esz[y.dtype],
+              "wgradpro": x.numel() // x.shape[-1] * (ci * 2) + gy.numel() // gy.shape[-1] * (co * 2),
               "wgrad": x.numel() // x.shape[-1] * (ci * 2) + gy.numel() // gy.shape[-1] * (co * 2)}
     dw = torch.empty((co, ci, *k), device=dev)
     db = torch.empty(co, device=dev)
@@ -77,6 +78,8 @@ def main():
         "fwdpro": lambda: F.conv(x, wp, y, k, pad, bias=b, prologue=F.PRO_AFFINE_RELU, pro_scale=psc, pro_shift=psh),
         "res": lambda: F.conv(x, wp, y, k, pad, bias=b, out_scale=0.1, residual=res),
         "wgrad": lambda: F.conv_wgrad(x, gy, k, pad, dw, db),
+        "wgradpro": lambda: F.conv_wgrad(x, gy, k, pad, dw, db, prologue=F.PRO_AFFINE_RELU, pro_scale=psc,
+                                         pro_shift=psh),
         "dgrad": lambda: F.conv(gy, wp1, dx, k, dpad),
     }
     for name in args.what.split(","):

@@ -43,9 +43,10 @@ extern "C" int vsrk_conv_set_path(const char* path, int32_t mode) {
   if (p == "fast") g_fast_mode = mode;
   else if (p == "thin") vsrk_g_thin_mode = mode;
   else if (p == "wgrad_fast") vsrk_g_wgrad_fast_mode = mode;
+  else if (p == "wgrad_pipe") vsrk_g_wgrad_pipe_mode = mode;
   else if (p == "k3") vsrk_g_k3_mode = mode;
   else if (p == "pw") vsrk_g_pw_mode = mode;
-  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, k3, pw, thin, wgrad_fast)", path);
+  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, k3, pw, thin, wgrad_fast, wgrad_pipe)", path);
   return VSRK_OK;
 }
 

@@ -41,6 +41,7 @@ extern int vsrk_g_pw_mode;
 extern int vsrk_g_k3_mode;
 extern int vsrk_g_thin_mode;
 extern int vsrk_g_wgrad_fast_mode;
+extern int vsrk_g_wgrad_pipe_mode;
 // vsrk_conv_set_grid_cap: > 0 caps the workgroups of the persistent conv grids
 // and of the weight-gradient split (tests drive the multi-tile loops with it)
 extern int vsrk_g_grid_cap;
