@@ -253,3 +253,42 @@ def test_wgrad_pipe_matches_generic(case, dtype):
         assert (pw.double() - wr.grad).abs().max().item() <= 1e-2 * (1 + wr.grad.abs().max().item())
         if bias:
             assert (pb.double() - br.grad).abs().max().item() <= 1e-2 * (1 + br.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("r,f,ci", [(2, 64, 64), (2, 16, 16), (3, 32, 64)])
+def test_wgrad_pipe_subpixel_dy(dtype, r, f, ci):
+    """Pipelined wgrad of an up-sampler conv whose output gradient is read
+    through a sub-pixel view (edsr_net.py:55-64: conv -> PixelShuffle):
+    bitwise equal to the generic kernel, and within bf16/fp16 tolerance of
+    fp64 autograd through pixel_shuffle."""
+    g = torch.Generator().manual_seed(13)
+    n, h, w = 2, 18, 40
+    co = f * r * r
+    x = torch.randn((n, 1, h, w, ci), generator=g)
+    gy = torch.randn((n, f, h * r, w * r), generator=g)
+    xd = x.to(DEV, dtype)
+    gy_cl = gy.permute(0, 2, 3, 1).unsqueeze(1).contiguous().to(DEV, dtype)
+
+    def run(pipe, cap):
+        F.set_conv_path("wgrad_pipe", pipe)
+        F.set_grid_cap(cap)
+        try:
+            dw = torch.empty((co, ci, 1, 3, 3), device=DEV)
+            db = torch.empty(co, device=DEV)
+            F.conv_wgrad(xd, gy_cl, (1, 3, 3), (0, 1, 1), dw, db, perm_r=r, dy_shuffle=r)
+            return dw.cpu(), db.cpu()
+        finally:
+            F.set_conv_path("wgrad_pipe", -1)
+            F.set_grid_cap(0)
+
+    wr = torch.zeros((co, ci, 3, 3), dtype=torch.float64, requires_grad=True)
+    br = torch.zeros(co, dtype=torch.float64, requires_grad=True)
+    y = Fn.pixel_shuffle(Fn.conv2d(_q(x, dtype)[:, 0].permute(0, 3, 1, 2), wr, br, padding=1), r)
+    y.backward(_q(gy, dtype))
+    for cap in (0, 5):
+        pw, pb = run(1, cap)
+        gw, gb = run(0, cap)
+        assert torch.equal(pw, gw) and torch.equal(pb, gb), (r, f, cap, (pw - gw).abs().max().item())
+        assert (pw[:, :, 0].double() - wr.grad).abs().max().item() <= 1e-2 * (1 + wr.grad.abs().max().item())
+        assert (pb.double() - br.grad).abs().max().item() <= 1e-2 * (1 + br.grad.abs().max().item())

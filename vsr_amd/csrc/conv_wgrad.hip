@@ -364,12 +364,15 @@ static WgradPlan wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, cons
     const char* e = getenv("VSRK_WGRAD_TARGET");
     target = e ? std::max(64, atoi(e)) : 0;
   }
-  // 3-D (kd > 1) kernels prefer many more, shorter workgroups: the DUF
-  // 224->32 3x3x3 wgrad at 64 x 5 x 128 x 128 took 5.68 ms at 512, 3.87 ms
-  // at 4096 (64->32: flat); the 2-D EDSR 64->64 is fastest at 512.
-  const int base = d->kd > 1 ? 4096 : 512;
-  int want = target ? ceil_div(target, p.ncombos)
-                    : std::min(ceil_div(base, p.ncombos), std::max(ceil_div(p.ntiles, 16), ceil_div(256, p.ncombos)));
+  // 3-D (kd > 1): about 64 tiles per workgroup (at least one workgroup per
+  // CU).  The pipelined kernel's sweep (profiles/r2_wgrad_pipe_ab.txt): DUF
+  // 64->32 at 64 x 7 x 128 x 128 fastest at ~1024 workgroups (~84 tiles
+  // each), 224->32 at ~4096 (~60 tiles each); the 2-D EDSR 64->64 is fastest
+  // at 512.
+  int want;
+  if (target) want = ceil_div(target, p.ncombos);
+  else if (d->kd > 1) want = std::max(ceil_div(p.ntiles, 64), ceil_div(256, p.ncombos));
+  else want = std::min(ceil_div(512, p.ncombos), std::max(ceil_div(p.ntiles, 16), ceil_div(256, p.ncombos)));
   if (vsrk_g_grid_cap > 0) want = std::max(1, vsrk_g_grid_cap / p.ncombos);
   want = std::max(1, std::min(want, p.ntiles));
   p.tps = ceil_div(p.ntiles, want);

@@ -24,6 +24,7 @@
 //    16-bit packing is v_cvt_pk_{bf16,f16}_f32 on vector converts.
 #include "conv_common.h"
 
+
 namespace {
 using namespace vsrk_conv;
 
@@ -103,7 +104,9 @@ struct WpGeom {
   }
 };
 
-template <typename T, int NCO, int NCI, int PRO>
+// ABL (A/B builds only, VSRK_WP_EXP): 1 = no staging inside the tile loop,
+// 2 = no fragment reads / MFMAs (the ceilings of either half)
+template <typename T, int NCO, int NCI, int PRO, int ABL>
 __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) void conv_wgrad_pipe_kernel(
     WgradArgs a) {
   using G = WpGeom<NCO, NCI>;
@@ -135,19 +138,30 @@ __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) vo
   const int xdst = (xrem >> 2) * SLOTP * PB + (xrem & 3) * 16;
   const int ybase_vox = tid / YCPV, xbase_slot = tid / XCPV;
   constexpr int YVSTEP = GTHR / YCPV, XSSTEP = G::XSSTEP;
-  // byte offsets within an (n, d) slice, relative to the tile origin
+  // byte offsets within an (n, d) slice, relative to the tile origin.  A
+  // sub-pixel view (r > 1) keeps logical channel c = (i*r + j)*cphys + c' at
+  // physical (h*r + i, w*r + j, c'): an 8-channel chunk never straddles
+  // sub-pixels (cphys % 8 == 0), so (i, j, c') is a per-thread constant.
   const int ysh = (int)a.dy.sh * 2, ysw = (int)a.dy.sw * 2;
   const int xsh = (int)a.x.sh * 2, xsw = (int)a.x.sw * 2;
+  auto chan_off = [](const View& v, int c, int sh2, int sw2) {
+    if (v.r == 1) return c * 2;
+    const int sub = c / v.cphys, cc = c - sub * v.cphys;
+    const int i = sub / v.r, j = sub - i * v.r;
+    return i * sh2 + j * sw2 + cc * 2;
+  };
+  const int ycoff = chan_off(a.dy, yc_ok ? yc : 0, ysh, ysw), xcoff = chan_off(a.x, xc_ok ? xc : 0, xsh, xsw);
+  const int ysh_r = ysh * a.dy.r, ysw_r = ysw * a.dy.r, xsh_r = xsh * a.x.r, xsw_r = xsw * a.x.r;
   uint32_t yrel[MAXY], xrel[MAXX];
 #pragma unroll
   for (int i = 0; i < MAXY; ++i) {
     const int v = ybase_vox + i * YVSTEP;
-    yrel[i] = (uint32_t)((v / TW) * ysh + (v % TW) * ysw + yc * 2);
+    yrel[i] = (uint32_t)((v / TW) * ysh_r + (v % TW) * ysw_r + ycoff);
   }
 #pragma unroll
   for (int i = 0; i < MAXX; ++i) {
     const int s = xbase_slot + i * XSSTEP;
-    xrel[i] = (uint32_t)((s / HWd) * xsh + (s % HWd) * xsw + xc * 2);
+    xrel[i] = (uint32_t)((s / HWd) * xsh_r + (s % HWd) * xsw_r + xcoff);
   }
 
   // prologue constants of this thread's 8 input channels
@@ -164,15 +178,53 @@ __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) vo
   // ---- tile walk (valid tiles only: the depth tap must land inside x) ----
   const int t_begin = split * a.tiles_per_split;
   const int t_end = min(a.ntiles, t_begin + a.tiles_per_split);
-  const int hw_tiles = a.tiles_w * a.tiles_h;
-  auto next_valid = [&](int t) __attribute__((always_inline)) {
-    while (t < t_end) {
-      const int dz = (t / hw_tiles) % a.dy.d;
-      const int di = dz + kdi - a.pd;
-      if (di >= 0 && di < a.x.d) break;
-      ++t;
+  // a scalar cursor (tile index and its decoded coordinates) advanced with
+  // carries: no divisions per tile
+  struct Cur {
+    int t, tw, th, dz, nb;
+  };
+  auto decode = [&](int t) __attribute__((always_inline)) {
+    Cur c;
+    c.t = t;
+    c.tw = t % a.tiles_w;
+    t /= a.tiles_w;
+    c.th = t % a.tiles_h;
+    t /= a.tiles_h;
+    c.dz = t % a.dy.d;
+    c.nb = t / a.dy.d;
+    return c;
+  };
+  auto next_slab = [&](Cur& c) __attribute__((always_inline)) {
+    c.tw = 0;
+    c.th = 0;
+    if (++c.dz == a.dy.d) {
+      c.dz = 0;
+      ++c.nb;
     }
-    return t;
+  };
+  // the first valid tile at or after c (the depth tap must land inside x)
+  auto skip_invalid = [&](Cur& c) __attribute__((always_inline)) {
+    while (c.t < t_end) {
+      const int di = c.dz + kdi - a.pd;
+      if (di >= 0 && di < a.x.d) break;
+      c.t += (a.tiles_w - c.tw) + (a.tiles_h - 1 - c.th) * a.tiles_w;
+      next_slab(c);
+    }
+  };
+  auto advance = [&](Cur& c) __attribute__((always_inline)) {
+    if (c.t >= t_end) return;
+    ++c.t;
+    if (++c.tw == a.tiles_w) {
+      c.tw = 0;
+      if (++c.th == a.tiles_h) {
+        c.th = 0;
+        if (++c.dz == a.dy.d) {
+          c.dz = 0;
+          ++c.nb;
+        }
+      }
+    }
+    skip_invalid(c);
   };
 
   // per-tile scalar state of an in-flight load set
@@ -180,22 +232,15 @@ __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) vo
     Rsrc ry, rx;
     int h0, w0;  // dY origin; x origin is (h0 - ph, w0 - pw)
   };
-  auto tile_refs = [&](int t) __attribute__((always_inline)) {
+  auto tile_refs = [&](const Cur& c) __attribute__((always_inline)) {
     TileRefs r;
-    int b = t;
-    const int tw_i = b % a.tiles_w;
-    b /= a.tiles_w;
-    const int th_i = b % a.tiles_h;
-    b /= a.tiles_h;
-    const int dz = b % a.dy.d;
-    const int nb = b / a.dy.d;
-    const int di = dz + kdi - a.pd;
-    r.h0 = th_i * GTH;
-    r.w0 = tw_i * TW;
-    const char* yb = a.dy.ptr + ((int64_t)nb * a.dy.sn + (int64_t)dz * a.dy.sd) * 2 +
-                     ((int64_t)r.h0 * a.dy.sh + (int64_t)r.w0 * a.dy.sw) * 2;
-    const char* xb = a.x.ptr + ((int64_t)nb * a.x.sn + (int64_t)di * a.x.sd) * 2 +
-                     ((int64_t)(r.h0 - a.ph) * a.x.sh + (int64_t)(r.w0 - a.pw) * a.x.sw) * 2;
+    const int di = c.dz + kdi - a.pd;
+    r.h0 = c.th * GTH;
+    r.w0 = c.tw * TW;
+    const char* yb = a.dy.ptr + ((int64_t)c.nb * a.dy.sn + (int64_t)c.dz * a.dy.sd) * 2 +
+                     ((int64_t)r.h0 * a.dy.sh + (int64_t)r.w0 * a.dy.sw) * 2 * a.dy.r;
+    const char* xb = a.x.ptr + ((int64_t)c.nb * a.x.sn + (int64_t)di * a.x.sd) * 2 +
+                     ((int64_t)(r.h0 - a.ph) * a.x.sh + (int64_t)(r.w0 - a.pw) * a.x.sw) * 2 * a.x.r;
     r.ry = rsrc_at(yb);
     r.rx = rsrc_at(xb);
     return r;
@@ -207,14 +252,14 @@ __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) vo
   auto load_chunk = [&](int i, const TileRefs& r, bool live) __attribute__((always_inline)) -> uint4 {
     if (i < MAXY) {
       const int v = ybase_vox + i * YVSTEP;
-      const bool ok = live && yc_ok && (unsigned)(r.h0 + v / TW) < (unsigned)a.dy.h &&
-                      (unsigned)(r.w0 + v % TW) < (unsigned)a.dy.w;
+      const bool ok = live & yc_ok & ((unsigned)(r.h0 + v / TW) < (unsigned)a.dy.h) &
+                      ((unsigned)(r.w0 + v % TW) < (unsigned)a.dy.w);
       return bload16(r.ry, ok ? yrel[i] : OOB);
     } else {
       const int j = i - MAXY;
       const int s = xbase_slot + j * XSSTEP;
-      const bool ok = live && xc_ok && s < SLOTS && (unsigned)(r.h0 - a.ph + s / HWd) < (unsigned)a.x.h &&
-                      (unsigned)(r.w0 - a.pw + s % HWd) < (unsigned)a.x.w;
+      const bool ok = live & xc_ok & (s < SLOTS) & ((unsigned)(r.h0 - a.ph + s / HWd) < (unsigned)a.x.h) &
+                      ((unsigned)(r.w0 - a.pw + s % HWd) < (unsigned)a.x.w);
       xm = (xm & ~(1u << j)) | ((ok ? 1u : 0u) << j);
       return bload16(r.rx, ok ? xrel[j] : OOB);
     }
@@ -257,56 +302,93 @@ __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) vo
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
 
   uint4 rg[NCH];
-  int t = next_valid(t_begin);
-  if (t >= t_end) t = t_end;
+  Cur c0 = decode(t_begin);
+  skip_invalid(c0);
+  const Cur cfirst = c0;  // a valid address for the dead loads past the end
   {
-    const TileRefs r0 = tile_refs(t < t_end ? t : t_begin);
+    const TileRefs r0 = tile_refs(c0.t < t_end ? c0 : cfirst);
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) rg[i] = load_chunk(i, r0, t < t_end);
+    for (int i = 0; i < NCH; ++i) rg[i] = load_chunk(i, r0, c0.t < t_end);
 #pragma unroll
     for (int i = 0; i < MAXY; ++i) commit_y(i, rg[i], lds);
 #pragma unroll
     for (int j = 0; j < MAXX; ++j) commit_x(j, rg[MAXY + j], lds);
   }
-  int tn = t < t_end ? next_valid(t + 1) : t_end;
-  TileRefs rn = tile_refs(tn < t_end ? tn : t_begin);
+  Cur c1 = c0;
+  advance(c1);
+  TileRefs rn = tile_refs(c1.t < t_end ? c1 : cfirst);
 #pragma unroll
-  for (int i = 0; i < NCH; ++i) rg[i] = load_chunk(i, rn, tn < t_end);
+  for (int i = 0; i < NCH; ++i) rg[i] = load_chunk(i, rn, c1.t < t_end);
   __syncthreads();
 
   int stage_i = 0;
   const int g = lane >> 4, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
   const int hfk = g >> 1, colb = ((g & 1) * 16 + 4 * p) * 2;
-  while (t < t_end) {
+  constexpr int ROWS = VPW / TW;           // dY rows of a wave's voxel part
+  constexpr int NSTEP = (ROWS + KK - 1) * 2;  // (input row, half) steps per tile
+  const int vr0 = vp * ROWS;
+  while (c0.t < t_end) {
     const char* cur = lds + stage_i * STAGE;
     char* nxt = lds + (stage_i ^ 1) * STAGE;
-    const int tnn = tn < t_end ? next_valid(tn + 1) : t_end;
-    const bool have_nn = tnn < t_end;
-    const TileRefs rnn = tile_refs(have_nn ? tnn : t_begin);
+    Cur c2 = c1;
+    advance(c2);
+    const bool have_nn = c2.t < t_end;
+    const TileRefs rnn = tile_refs(have_nn ? c2 : cfirst);
     const char* py = cur + cos_ * VOX * PB;
     const char* px = cur + YBYTES + cis * SLOTP * PB;
+    // Row-reuse walk: a wave holds the dY fragments of its ROWS rows (both
+    // 16-voxel halves) and walks the XR = ROWS + 2 input rows once; each
+    // input fragment (row xr, half c, tap kw) serves every kh with dY row
+    // xr - kh inside the wave's rows.  Per accumulator the MFMA order is
+    // still (dY row, half) ascending, as in conv_wgrad_kernel.
+    uint4 fa[ROWS][2];
+    if constexpr (!(ABL & 2)) {
 #pragma unroll
-    for (int ks = 0; ks < KSTEPS; ++ks) {
-      const int vb = vp * VPW + ks * 16;
-      const int vrow = vb / TW, vcol0 = (vb % TW) + 8 * hfk;
-      v4i16 y0 = ds_read_tr(py + (vrow * TW + vcol0 + q) * PB + colb);
-      v4i16 y1 = ds_read_tr(py + (vrow * TW + vcol0 + 4 + q) * PB + colb);
-      const uint4 af = __builtin_bit_cast(uint4, __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7));
+      for (int r = 0; r < ROWS; ++r)
 #pragma unroll
-      for (int khi = 0; khi < KK; ++khi) {
+        for (int c = 0; c < 2; ++c) {
+          const char* ys = py + ((vr0 + r) * TW + c * 16 + 8 * hfk + q) * PB + colb;
+          const v4i16 y0 = ds_read_tr(ys);
+          const v4i16 y1 = ds_read_tr(ys + 4 * PB);
+          fa[r][c] = __builtin_bit_cast(uint4, __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+    }
+    // input fragments are software-pipelined one step ahead: the reads of
+    // step st + 1 are issued (fenced from the scheduler) before step st's
+    // MFMAs, which consume the reads issued one step earlier
+    auto read_b = [&](int st, uint4* fb) __attribute__((always_inline)) {
+      const int xr = st >> 1, c = st & 1;
 #pragma unroll
-        for (int kwi = 0; kwi < KK; ++kwi) {
-          const char* xs = px + ((vrow + khi) * HWd + vcol0 + kwi + q) * PB + colb;
-          v4i16 x0 = ds_read_tr(xs);
-          v4i16 x1 = ds_read_tr(xs + 4 * PB);
-          const uint4 bfr = __builtin_bit_cast(uint4, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
-          mma<T>(acc[khi * KK + kwi], af, bfr);
+      for (int kwi = 0; kwi < KK; ++kwi) {
+        const char* xs = px + ((vr0 + xr) * HWd + c * 16 + 8 * hfk + kwi + q) * PB + colb;
+        const v4i16 x0 = ds_read_tr(xs);
+        const v4i16 x1 = ds_read_tr(xs + 4 * PB);
+        fb[kwi] = __builtin_bit_cast(uint4, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+    };
+    uint4 fbuf[2][KK];
+    if constexpr (!(ABL & 2)) read_b(0, fbuf[0]);
+#pragma unroll
+    for (int st = 0; st < NSTEP; ++st) {
+      const int xr = st >> 1, c = st & 1;
+      if constexpr (!(ABL & 2)) {
+        if (st + 1 < NSTEP) read_b(st + 1, fbuf[(st + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint4* fb = fbuf[st & 1];
+#pragma unroll
+        for (int khi = KK - 1; khi >= 0; --khi) {
+          const int r = xr - khi;
+          if (r >= 0 && r < ROWS) {
+#pragma unroll
+            for (int kwi = 0; kwi < KK; ++kwi) mma<T>(acc[khi * KK + kwi], fa[r][c], fb[kwi]);
+          }
         }
       }
+      if constexpr (!(ABL & 1)) {
       // stage tile t+1 into the other buffer and refill its registers with
-      // tile t+2: the dY chunks after the first k-step, the X chunks spread
-      // over the rest (a past-the-end tile stages zeros nobody reads)
-      if (ks == 0) {
+      // tile t+2: the dY chunks in the first step, the X chunks spread over
+      // the rest (a past-the-end tile stages zeros nobody reads)
+      if (st == 0) {
 #pragma unroll
         for (int i = 0; i < MAXY; ++i) {
           commit_y(i, rg[i], nxt);
@@ -315,16 +397,18 @@ __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) vo
       }
 #pragma unroll
       for (int j = 0; j < MAXX; ++j) {
-        if ((j * KSTEPS) / MAXX == ks) {
+        if ((j * NSTEP) / MAXX == st) {
           commit_x(j, rg[MAXY + j], nxt);
           rg[MAXY + j] = load_chunk(MAXY + j, rnn, have_nn);
         }
       }
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
     stage_i ^= 1;
-    t = tn;
-    tn = tnn;
+    c0 = c1;
+    c1 = c2;
     rn = rnn;
   }
 
@@ -386,27 +470,43 @@ __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) vo
 template <typename T, int NCO, int NCI, int PRO>
 void launch_pipe(const WgradArgs& a, hipStream_t s) {
   const size_t lds = WpGeom<NCO, NCI>::lds_bytes();
-  auto kern = conv_wgrad_pipe_kernel<T, NCO, NCI, PRO>;
+  auto kern = conv_wgrad_pipe_kernel<T, NCO, NCI, PRO, 0>;
+#ifdef VSRK_WP_EXP
+  static int abl = -1;
+  if (abl < 0) {
+    const char* e = getenv("VSRK_WP_ABLATE");
+    abl = e ? atoi(e) : 0;
+  }
+  if (abl == 1) kern = conv_wgrad_pipe_kernel<T, NCO, NCI, PRO, 1>;
+  if (abl == 2) kern = conv_wgrad_pipe_kernel<T, NCO, NCI, PRO, 2>;
+#endif
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   kern<<<a.nblk, GTHR, lds, s>>>(a);
 }
 
+// prologue: none or BN-affine+ReLU (the DUF conv2 input); other modes take
+// the generic kernel
 template <typename T, int NCO, int NCI>
-void pipe_pro(const WgradArgs& a, hipStream_t s) {
-  switch (a.prologue & (VSRK_PRO_AFFINE | VSRK_PRO_RELU)) {
-    case 0: launch_pipe<T, NCO, NCI, 0>(a, s); break;
-    case VSRK_PRO_RELU: launch_pipe<T, NCO, NCI, VSRK_PRO_RELU>(a, s); break;
-    case VSRK_PRO_AFFINE: launch_pipe<T, NCO, NCI, VSRK_PRO_AFFINE>(a, s); break;
-    default: launch_pipe<T, NCO, NCI, VSRK_PRO_AFFINE | VSRK_PRO_RELU>(a, s); break;
-  }
+bool pipe_pro(const WgradArgs& a, hipStream_t s) {
+  const int pro = a.prologue & (VSRK_PRO_AFFINE | VSRK_PRO_RELU);
+  if (pro == 0) launch_pipe<T, NCO, NCI, 0>(a, s);
+  else if (pro == (VSRK_PRO_AFFINE | VSRK_PRO_RELU)) launch_pipe<T, NCO, NCI, VSRK_PRO_AFFINE | VSRK_PRO_RELU>(a, s);
+  else return false;
+  return true;
 }
 
 template <typename T>
-void pipe_t(const WgradArgs& a, int nco, int nci, hipStream_t s) {
-  if (nco == 2 && nci == 2) pipe_pro<T, 2, 2>(a, s);
-  else if (nco == 2) pipe_pro<T, 2, 1>(a, s);
-  else if (nci == 2) pipe_pro<T, 1, 2>(a, s);
-  else pipe_pro<T, 1, 1>(a, s);
+bool pipe_t(const WgradArgs& a, int nco, int nci, hipStream_t s) {
+#ifdef VSRK_WP_EXP
+  if (nco == 1 && nci == 2) return pipe_pro<T, 1, 2>(a, s);
+  if (nco == 2 && nci == 2) return pipe_pro<T, 2, 2>(a, s);
+  return false;
+#else
+  if (nco == 2 && nci == 2) return pipe_pro<T, 2, 2>(a, s);
+  if (nco == 2) return pipe_pro<T, 2, 1>(a, s);
+  if (nci == 2) return pipe_pro<T, 1, 2>(a, s);
+  return pipe_pro<T, 1, 1>(a, s);
+#endif
 }
 
 }  // namespace
@@ -423,19 +523,21 @@ bool vsrk_wgrad_pipe_enabled() {
 }
 
 // 1 = launched (same slab layout as conv_wgrad_kernel); 0 = not eligible.
-// Eligible: 16-bit, kh = kw = 3, plain (non-sub-pixel) chunk-readable views,
-// whole 16-byte channel chunks, an (n, d) slice addressable in 31 bits.
+// Eligible: 16-bit, kh = kw = 3, chunk-readable views (plain or sub-pixel),
+// whole 16-byte channel chunks, an (n, d) slice addressable in 30 bits.
 int vsrk_conv_wgrad_pipe(const WgradArgs& a, int nco, int nci, int dtype, hipStream_t s) {
   if (!vsrk_wgrad_pipe_enabled()) return 0;
   if (a.kh != 3 || a.kw != 3) return 0;
-  if (a.x.r > 1 || a.dy.r > 1 || !a.xvec || !a.dyvec) return 0;
-  if (a.cin % 8 || a.cout % 8) return 0;
-  const int64_t xs = ((int64_t)a.x.h * a.x.sh + (int64_t)a.x.w * a.x.sw) * 2;
-  const int64_t ys = ((int64_t)a.dy.h * a.dy.sh + (int64_t)a.dy.w * a.dy.sw) * 2;
+  if (!a.xvec || !a.dyvec) return 0;
+  if (a.cin % 8 || a.cout % 8 || a.x.cphys % 8 || a.dy.cphys % 8) return 0;
+  const int64_t xs = ((int64_t)a.x.h * a.x.sh + (int64_t)a.x.w * a.x.sw) * 2 * a.x.r * a.x.r;
+  const int64_t ys = ((int64_t)a.dy.h * a.dy.sh + (int64_t)a.dy.w * a.dy.sw) * 2 * a.dy.r * a.dy.r;
   if (xs >= (1ll << 30) || ys >= (1ll << 30)) return 0;
   if (a.x.sh < 0 || a.x.sw < 0 || a.dy.sh < 0 || a.dy.sw < 0) return 0;
-  if (dtype == VSRK_BF16) pipe_t<bf16>(a, nco, nci, s);
-  else if (dtype == VSRK_F16) pipe_t<f16>(a, nco, nci, s);
-  else return 0;
-  return 1;
+  bool ok = false;
+  if (dtype == VSRK_BF16) ok = pipe_t<bf16>(a, nco, nci, s);
+#ifndef VSRK_WP_EXP
+  else if (dtype == VSRK_F16) ok = pipe_t<f16>(a, nco, nci, s);
+#endif
+  return ok ? 1 : 0;
 }
