@@ -238,6 +238,13 @@ int vsrk_ssim3d(const float* out, const float* target, int32_t batch, int32_t ch
  * so a data-parallel caller can all-reduce the per-channel sums between the
  * calls (SyncBatchNorm):
  *   vsrk_bn_stats:    sum, sumsq over every voxel of x (channels-last view)
+ *   vsrk_bn_stats_grouped: the same per group of rows: x's (n, d, h) rows,
+ *                     n outermost, split into `groups` equal runs; sum and
+ *                     sumsq are [groups][C].  With x a depth-major view
+ *                     (n := depth) this is the per-depth statistics of a
+ *                     concat-buffer slice, which DUF's dense layer reuses
+ *                     for every later BatchNorm over the same channels
+ *                     (duf_net.py:122-128: concat channels never change)
  *   vsrk_bn_finalize: mean, biased var -> scale = gamma*invstd,
  *                     shift = beta - mean*scale (the fused conv prologue's
  *                     VSRK_PRO_AFFINE_RELU operands), running stats updated
@@ -257,6 +264,8 @@ int vsrk_ssim3d(const float* out, const float* target, int32_t batch, int32_t ch
 size_t vsrk_bn_workspace_size(int32_t channels);
 int vsrk_bn_stats(const vsrk_tensor5* x, float* sum, float* sumsq, void* workspace, size_t workspace_bytes,
                   void* stream);
+int vsrk_bn_stats_grouped(const vsrk_tensor5* x, int32_t groups, float* sum, float* sumsq, void* workspace,
+                          size_t workspace_bytes, void* stream);
 int vsrk_bn_finalize(const float* sum, const float* sumsq, double count, const float* gamma, const float* beta,
                      float eps, float momentum, float* running_mean, float* running_var, float* scale,
                      float* shift, float* mean, float* invstd, int32_t channels, void* stream);

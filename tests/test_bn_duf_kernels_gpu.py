@@ -17,6 +17,24 @@ def _rel(a, b):
     return (a.double().cpu() - b.double().cpu()).norm().item() / max(b.double().norm().item(), 1e-30)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("c", [32, 64, 200])
+def test_bn_stats_depth(dtype, c):
+    """Per-depth statistics of a depth window / channel slice of a concat
+    buffer (the DUF bn1 cache) vs fp64, and their sum vs the one-pass stats."""
+    g = torch.Generator().manual_seed(7 + c)
+    big = torch.randn((3, 7, 11, 37, c + 40), generator=g) * 1.5 + 0.3
+    xd = big.to(DEV, dtype)[:, 1:6, :, :, 16:16 + c]
+    xq = big.to(dtype).double()[:, 1:6, :, :, 16:16 + c]
+    sd = F.bn_stats_depth(xd)
+    assert sd.shape == (5, 2, c)
+    ref1 = xq.sum(dim=(0, 2, 3))
+    ref2 = (xq * xq).sum(dim=(0, 2, 3))
+    assert _rel(sd[:, 0], ref1) <= 1e-5 and _rel(sd[:, 1], ref2) <= 1e-5
+    whole = F.bn_stats(xd)
+    assert _rel(sd.double().sum(0), whole) <= 1e-5
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("c", [32, 160, 224])
 def test_bn_forward_stats_and_running(dtype, c):

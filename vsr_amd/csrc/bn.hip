@@ -15,7 +15,7 @@
 
 namespace {
 
-constexpr int RB = 512;  // reduction blocks (partials)
+constexpr int RB = 2048;  // reduction blocks (partials): 8 per CU
 
 // Row decomposition: a "row" is one (n, d, h) line of W voxels.  Threads are
 // (voxel lane vl, chunk position ch) with ch fixed for the launch, so a
@@ -38,8 +38,8 @@ template <typename T, int MODE>
 __global__ __launch_bounds__(256) void chan_reduce_kernel(View x, View dz, const float* __restrict__ scale,
                                                           const float* __restrict__ shift,
                                                           const float* __restrict__ mean,
-                                                          const float* __restrict__ invstd, int nrows, int rpb,
-                                                          float* __restrict__ part) {
+                                                          const float* __restrict__ invstd, int rpg, int bpg,
+                                                          int rpb, float* __restrict__ part) {
   constexpr int E = Chunk<T>::E;
   const int C = x.c;
   const int cpv = (C + E - 1) / E;  // chunks per voxel
@@ -61,39 +61,60 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(View x, View dz, const
     }
   }
   if (vl < vpb) {
-    const int r0 = blockIdx.x * rpb, r1 = min(nrows, r0 + rpb);
+    // rows of group g = blockIdx / bpg are [g*rpg, (g+1)*rpg); this block
+    // takes its rpb-row share of them
+    const int g = blockIdx.x / bpg, bi = blockIdx.x - g * bpg;
+    const int r0 = g * rpg + min(rpg, bi * rpb), r1 = g * rpg + min(rpg, (bi + 1) * rpb);
+    // U voxels per thread per pass, all loads issued before any is used:
+    // U (stats) or 2U (backward) 16-byte loads in flight per thread.  One
+    // load at a time (the first version) streamed at ~3.1 TB/s.
+    constexpr int U = 4;
     for (int r = r0; r < r1; ++r) {
       const T* xr = reinterpret_cast<const T*>(x.ptr) + row_off(x, r) + c0;
       const T* gr = MODE == 1 ? reinterpret_cast<const T*>(dz.ptr) + row_off(dz, r) + c0 : nullptr;
-      for (int w = vl; w < x.w; w += vpb) {
-        float f[E];
-        const T* px = xr + (int64_t)w * x.sw;
-        if (full) {
-          Chunk<T>::unpack(*reinterpret_cast<const uint4*>(px), f);
-        } else {
+      for (int wb = vl; wb < x.w; wb += U * vpb) {
+        uint4 rx[U], rg[U];
 #pragma unroll
-          for (int e = 0; e < E; ++e) f[e] = c0 + e < C ? to_f32<T>(px[e]) : 0.f;
-        }
-        if (MODE == 0) {
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            s1[e] += f[e];
-            s2[e] = fmaf(f[e], f[e], s2[e]);
+        for (int u = 0; u < U; ++u) {
+          const int w = wb + u * vpb;
+          rx[u] = make_uint4(0, 0, 0, 0);
+          rg[u] = make_uint4(0, 0, 0, 0);
+          if (full && w < x.w) {
+            rx[u] = *reinterpret_cast<const uint4*>(xr + (int64_t)w * x.sw);
+            if (MODE == 1) rg[u] = *reinterpret_cast<const uint4*>(gr + (int64_t)w * dz.sw);
           }
-        } else {
-          float g[E];
-          const T* pg = gr + (int64_t)w * dz.sw;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int w = wb + u * vpb;
+          if (w >= x.w) break;
+          float f[E], g[E];
           if (full) {
-            Chunk<T>::unpack(*reinterpret_cast<const uint4*>(pg), g);
+            Chunk<T>::unpack(rx[u], f);
+            if (MODE == 1) Chunk<T>::unpack(rg[u], g);
+          } else {
+            const T* px = xr + (int64_t)w * x.sw;
+#pragma unroll
+            for (int e = 0; e < E; ++e) f[e] = c0 + e < C ? to_f32<T>(px[e]) : 0.f;
+            if (MODE == 1) {
+              const T* pg = gr + (int64_t)w * dz.sw;
+#pragma unroll
+              for (int e = 0; e < E; ++e) g[e] = c0 + e < C ? to_f32<T>(pg[e]) : 0.f;
+            }
+          }
+          if (MODE == 0) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+              s1[e] += f[e];
+              s2[e] = fmaf(f[e], f[e], s2[e]);
+            }
           } else {
 #pragma unroll
-            for (int e = 0; e < E; ++e) g[e] = c0 + e < C ? to_f32<T>(pg[e]) : 0.f;
-          }
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            const float dy = fmaf(f[e], sc[e], sh[e]) > 0.f ? g[e] : 0.f;
-            s1[e] += dy;
-            s2[e] = fmaf(dy, (f[e] - mu[e]) * is[e], s2[e]);
+            for (int e = 0; e < E; ++e) {
+              const float dy = fmaf(f[e], sc[e], sh[e]) > 0.f ? g[e] : 0.f;
+              s1[e] += dy;
+              s2[e] = fmaf(dy, (f[e] - mu[e]) * is[e], s2[e]);
+            }
           }
         }
       }
@@ -126,11 +147,13 @@ __global__ __launch_bounds__(256) void chan_reduce_kernel(View x, View dz, const
 // double, then a fixed-shape tree (deterministic).  The first version ran one
 // thread per channel over all partials serially (133 us per call, 26 calls
 // per DUF step).
-__global__ __launch_bounds__(256) void chan_final_kernel(const float* __restrict__ part, int nblk, int C,
+__global__ __launch_bounds__(256) void chan_final_kernel(const float* __restrict__ part, int bpg, int C,
                                                          float* __restrict__ o1, float* __restrict__ o2) {
-  const int c = blockIdx.x, t = threadIdx.x;
+  // block (c, g): channel c of row group g, whose partials are blocks
+  // [g*bpg, (g+1)*bpg)
+  const int c = blockIdx.x, g = blockIdx.y, t = threadIdx.x;
   double a = 0.0, b = 0.0;
-  for (int k = t; k < nblk; k += 256) {
+  for (int k = g * bpg + t; k < (g + 1) * bpg; k += 256) {
     a += part[((int64_t)k * 2) * C + c];
     b += part[((int64_t)k * 2 + 1) * C + c];
   }
@@ -146,8 +169,8 @@ __global__ __launch_bounds__(256) void chan_final_kernel(const float* __restrict
     __syncthreads();
   }
   if (t == 0) {
-    o1[c] = (float)ra[0];
-    o2[c] = (float)rb[0];
+    o1[(int64_t)g * C + c] = (float)ra[0];
+    o2[(int64_t)g * C + c] = (float)rb[0];
   }
 }
 
@@ -225,37 +248,56 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(View x, View dz,
     const T* xr = reinterpret_cast<const T*>(x.ptr) + row_off(x, r) + c0;
     const T* gr = reinterpret_cast<const T*>(dz.ptr) + row_off(dz, r) + c0;
     T* orow = reinterpret_cast<T*>(dx.ptr) + row_off(dx, r) + c0;
-    for (int w = vl; w < x.w; w += vpb) {
-      const T* px = xr + (int64_t)w * x.sw;
-      const T* pg = gr + (int64_t)w * dz.sw;
-      T* po = orow + (int64_t)w * dx.sw;
-      float f[E], g[E], o[E];
-      if (full) {
-        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(px), f);
-        Chunk<T>::unpack(*reinterpret_cast<const uint4*>(pg), g);
-        if (accumulate) Chunk<T>::unpack(*reinterpret_cast<const uint4*>(po), o);
-      } else {
+    // U voxels per pass, every load issued before any is used (up to 3U
+    // 16-byte loads in flight per thread)
+    constexpr int U = 2;
+    for (int wb = vl; wb < x.w; wb += U * vpb) {
+      uint4 rx[U], rg[U], ro[U];
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const bool ok = c0 + e < C;
-          f[e] = ok ? to_f32<T>(px[e]) : 0.f;
-          g[e] = ok ? to_f32<T>(pg[e]) : 0.f;
-          o[e] = (ok && accumulate) ? to_f32<T>(po[e]) : 0.f;
+      for (int u = 0; u < U; ++u) {
+        const int w = wb + u * vpb;
+        rx[u] = rg[u] = ro[u] = make_uint4(0, 0, 0, 0);
+        if (full && w < x.w) {
+          rx[u] = *reinterpret_cast<const uint4*>(xr + (int64_t)w * x.sw);
+          rg[u] = *reinterpret_cast<const uint4*>(gr + (int64_t)w * dz.sw);
+          if (accumulate) ro[u] = *reinterpret_cast<const uint4*>(orow + (int64_t)w * dx.sw);
         }
       }
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const float dy = fmaf(f[e], sc[e], sh[e]) > 0.f ? g[e] : 0.f;
-        float rr = fmaf(k1[e], dy, fmaf(k2[e], f[e], k3[e]));
-        if (accumulate) rr += o[e];
-        o[e] = rr;
-      }
-      if (full) {
-        *reinterpret_cast<uint4*>(po) = Chunk<T>::pack(o);
-      } else {
+      for (int u = 0; u < U; ++u) {
+        const int w = wb + u * vpb;
+        if (w >= x.w) break;
+        const T* px = xr + (int64_t)w * x.sw;
+        const T* pg = gr + (int64_t)w * dz.sw;
+        T* po = orow + (int64_t)w * dx.sw;
+        float f[E], g[E], o[E];
+        if (full) {
+          Chunk<T>::unpack(rx[u], f);
+          Chunk<T>::unpack(rg[u], g);
+          Chunk<T>::unpack(ro[u], o);
+        } else {
 #pragma unroll
-        for (int e = 0; e < E; ++e)
-          if (c0 + e < C) po[e] = from_f32<T>(o[e]);
+          for (int e = 0; e < E; ++e) {
+            const bool ok = c0 + e < C;
+            f[e] = ok ? to_f32<T>(px[e]) : 0.f;
+            g[e] = ok ? to_f32<T>(pg[e]) : 0.f;
+            o[e] = (ok && accumulate) ? to_f32<T>(po[e]) : 0.f;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float dy = fmaf(f[e], sc[e], sh[e]) > 0.f ? g[e] : 0.f;
+          float rr = fmaf(k1[e], dy, fmaf(k2[e], f[e], k3[e]));
+          if (accumulate) rr += o[e];
+          o[e] = rr;
+        }
+        if (full) {
+          *reinterpret_cast<uint4*>(po) = Chunk<T>::pack(o);
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e)
+            if (c0 + e < C) po[e] = from_f32<T>(o[e]);
+        }
       }
     }
   }
@@ -312,7 +354,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(View x, View y, const flo
 
 int reduce_launch(int mode, const vsrk_tensor5* x, const vsrk_tensor5* dz, const float* scale, const float* shift,
                   const float* mean, const float* invstd, float* o1, float* o2, void* ws, size_t ws_bytes,
-                  hipStream_t s) {
+                  hipStream_t s, int groups = 1) {
   const int E = vsrk_is16(x->dtype) ? 8 : 4;
   const int cpv = ceil_div(x->c, E);
   VSRK_CHECK(cpv <= 256, "bn: too many channels (%d)", x->c);
@@ -320,29 +362,34 @@ int reduce_launch(int mode, const vsrk_tensor5* x, const vsrk_tensor5* dz, const
   const int64_t nr64 = (int64_t)x->n * x->d * x->h;
   VSRK_CHECK(nr64 < (1ll << 31), "bn: too many rows");
   const int nrows = (int)nr64;
-  const int rpb = std::max(1, ceil_div(nrows, RB));
-  const int nblk = std::max(1, ceil_div(nrows, rpb));
+  VSRK_CHECK(groups >= 1 && groups <= RB && nrows % groups == 0, "bn: %d rows do not split into %d groups", nrows,
+             groups);
+  const int rpg = nrows / groups;
+  const int bpg = std::max(1, std::min(rpg, RB / groups));  // blocks per group
+  const int rpb = std::max(1, ceil_div(rpg, bpg));
+  const int nblk = groups * bpg;
   const size_t need = (size_t)nblk * 2 * x->c * sizeof(float);
   VSRK_CHECK(ws && ws_bytes >= need, "bn: workspace %zu < %zu bytes", ws_bytes, need);
   VSRK_CHECK(x->shuffle <= 1 && (!dz || (dz->shuffle <= 1 && dz->n == x->n && dz->d == x->d && dz->h == x->h &&
                                          dz->w == x->w)),
              "bn: sub-pixel views / mismatched x, dz shapes are not supported");
+  if (nrows == 0) return VSRK_OK;
   View vx = make_view(x);
   View vg = dz ? make_view(dz) : vx;
   float* part = (float*)ws;
   const int thr = cpv * vpb;
   if (x->dtype == VSRK_BF16) {
-    if (mode == 0) chan_reduce_kernel<bf16, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
-    else chan_reduce_kernel<bf16, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
+    if (mode == 0) chan_reduce_kernel<bf16, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, rpg, bpg, rpb, part);
+    else chan_reduce_kernel<bf16, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, rpg, bpg, rpb, part);
   } else if (x->dtype == VSRK_F16) {
-    if (mode == 0) chan_reduce_kernel<f16, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
-    else chan_reduce_kernel<f16, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
+    if (mode == 0) chan_reduce_kernel<f16, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, rpg, bpg, rpb, part);
+    else chan_reduce_kernel<f16, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, rpg, bpg, rpb, part);
   } else {
-    if (mode == 0) chan_reduce_kernel<float, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
-    else chan_reduce_kernel<float, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, nrows, rpb, part);
+    if (mode == 0) chan_reduce_kernel<float, 0><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, rpg, bpg, rpb, part);
+    else chan_reduce_kernel<float, 1><<<nblk, thr, 0, s>>>(vx, vg, scale, shift, mean, invstd, rpg, bpg, rpb, part);
   }
   VSRK_LAUNCH_CHECK("bn_reduce");
-  chan_final_kernel<<<x->c, 256, 0, s>>>(part, nblk, x->c, o1, o2);
+  chan_final_kernel<<<dim3(x->c, groups), 256, 0, s>>>(part, bpg, x->c, o1, o2);
   VSRK_LAUNCH_CHECK("bn_reduce_final");
   return VSRK_OK;
 }
@@ -356,6 +403,13 @@ extern "C" int vsrk_bn_stats(const vsrk_tensor5* x, float* sum, float* sumsq, vo
   VSRK_CHECK(x && x->ptr && sum && sumsq, "bn_stats: null argument");
   return reduce_launch(0, x, nullptr, nullptr, nullptr, nullptr, nullptr, sum, sumsq, workspace, workspace_bytes,
                        (hipStream_t)stream);
+}
+
+extern "C" int vsrk_bn_stats_grouped(const vsrk_tensor5* x, int32_t groups, float* sum, float* sumsq,
+                                     void* workspace, size_t workspace_bytes, void* stream) {
+  VSRK_CHECK(x && x->ptr && sum && sumsq, "bn_stats_grouped: null argument");
+  return reduce_launch(0, x, nullptr, nullptr, nullptr, nullptr, nullptr, sum, sumsq, workspace, workspace_bytes,
+                       (hipStream_t)stream, groups);
 }
 
 extern "C" int vsrk_bn_finalize(const float* sum, const float* sumsq, double count, const float* gamma,

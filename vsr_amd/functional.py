@@ -311,6 +311,20 @@ def bn_stats(x: torch.Tensor):
     return out
 
 
+def bn_stats_depth(x: torch.Tensor) -> torch.Tensor:
+    """Per-depth per-channel (sum, sumsq) of a channels-last (N, D, H, W, C)
+    view -> (D, 2, C) fp32.  One launch: rows are walked depth-major and each
+    depth's partials are reduced on their own (vsrk_bn_stats_grouped)."""
+    lib = _lib()
+    d, c = x.shape[1], x.shape[-1]
+    out = torch.empty((2, d, c), dtype=torch.float32, device=x.device)
+    xv = N.t5(x.transpose(0, 1))  # n := depth, so depth d owns one contiguous run of rows
+    ws = _bn_ws(c, x.device)
+    N.check(lib.vsrk_bn_stats_grouped(C.byref(xv), d, out[0].data_ptr(), out[1].data_ptr(), ws.data_ptr(),
+                                      ws.numel(), N.stream_ptr(x.device)), "bn_stats_grouped")
+    return out.transpose(0, 1)
+
+
 def bn_finalize(sums: torch.Tensor, count: float, gamma, beta, eps: float, momentum: float,
                 running_mean=None, running_var=None) -> torch.Tensor:
     """-> (4, C) fp32: scale, shift, mean, invstd (running stats updated in place)."""

@@ -93,15 +93,19 @@ class DUFNet(BaseNet):
         return n // 2 if n % 2 == 1 else n // 2 - 1  # duf_net.py:53
 
     # -- BatchNorm helpers ------------------------------------------------
-    def _bn_forward(self, bn: nn.BatchNorm3d, x: torch.Tensor) -> torch.Tensor:
-        """(4, C) = scale, shift, mean, invstd for the fused BN+ReLU prologue."""
+    def _bn_forward(self, bn: nn.BatchNorm3d, x: torch.Tensor, sums: torch.Tensor | None = None) -> torch.Tensor:
+        """(4, C) = scale, shift, mean, invstd for the fused BN+ReLU prologue.
+        sums: x's per-channel (sum, sumsq) when the caller already has them."""
         if not self.training:
             # running statistics; the backward (a gradient taken through an
             # eval-mode net) then has no batch-statistics terms: count = inf
             st = F.bn_fold_running(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
             st.count = float("inf")
             return st
-        sums = F.bn_stats(x)
+        if sums is None:
+            sums = F.bn_stats(x)
+        else:
+            sums = sums.clone()  # the SyncBN hook all-reduces in place
         count = x.shape[0] * x.shape[1] * x.shape[2] * x.shape[3]
         if self.bn_allreduce is not None:
             count *= self.bn_allreduce(sums)
@@ -149,13 +153,25 @@ class DUFNet(BaseNet):
         xv = F.to_view(frames, cd, cpad=8)[..., :cin]  # (n, T, h, w, cin), chunk-aligned storage
         C = torch.empty((n, T, h, w, ctot), dtype=cd, device=dev)
         F.conv(xv, F.pack_weight(self.head.weight, 0, cd), C[..., :64], (1, 3, 3), (0, 1, 1), bias=self.head.bias)
+        # Per-depth (sum, sumsq) of every channel of C, taken once when the
+        # channel slice is written: the concat channels never change, so each
+        # unit's bn1 (and the tail bn) over a depth window of C[..., :f] is a
+        # sum of these rows instead of another pass over f channels.
+        S = None
+        if self.training:
+            S = torch.empty((T, 2, ctot), dtype=torch.float32, device=dev)
+            S[:, :, :64] = F.bn_stats_depth(C[..., :64])
+
+        def window_sums(lo_, hi_, c_):
+            return None if S is None else S[lo_:hi_, :, :c_].double().sum(0).float()
+
         units = []
         lo, hi, f = 0, T, 64
         for i in range(dl.n_units):
             u = getattr(dl, f"conv{i}")
             keep = i < dl.n_keep
             R = C[:, lo:hi, :, :, :f]
-            st1 = self._bn_forward(u.bn1, R)
+            st1 = self._bn_forward(u.bn1, R, window_sums(lo, hi, f))
             t1 = torch.empty((n, hi - lo, h, w, f), dtype=cd, device=dev)
             F.conv(R, F.pack_weight(u.conv1.weight, 0, cd), t1, (1, 1, 1), (0, 0, 0), bias=u.conv1.bias,
                    prologue=ARF, pro_scale=st1[0], pro_shift=st1[1])
@@ -164,10 +180,12 @@ class DUFNet(BaseNet):
             pad = (1, 1, 1) if keep else (0, 1, 1)
             F.conv(t1, F.pack_weight(u.conv2.weight, 0, cd), C[:, olo:ohi, :, :, f:f + g], (3, 3, 3), pad,
                    bias=u.conv2.bias, prologue=ARF, pro_scale=st2[0], pro_shift=st2[1])
+            if S is not None:
+                S[olo:ohi, :, f:f + g] = F.bn_stats_depth(C[:, olo:ohi, :, :, f:f + g])
             units.append((lo, hi, olo, ohi, f, pad, st1, st2, t1))
             lo, hi, f = olo, ohi, f + g
         Rt = C[:, lo:hi, :, :, :ctot]  # depth window [3, 4) for T = 7
-        stt = self._bn_forward(dl.tail.bn, Rt)
+        stt = self._bn_forward(dl.tail.bn, Rt, window_sums(lo, hi, ctot))
         feat = torch.empty((n, 1, h, w, 256), dtype=cd, device=dev)
         F.conv(Rt, F.pack_weight(dl.tail.conv.weight, 0, cd), feat, (1, 3, 3), (0, 1, 1), bias=dl.tail.conv.bias,
                prologue=ARF, pro_scale=stt[0], pro_shift=stt[1])
