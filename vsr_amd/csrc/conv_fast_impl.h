@@ -74,6 +74,13 @@ int fast_k3_n64_ys(const FastArgs& a, bool yf, bool h16, hipStream_t s);        
 namespace {
 using namespace vsrk_conv;
 
+// s_waitcnt vmcnt(N) (expcnt / lgkmcnt left at their maxima)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
 // 16 B per lane of zeros: the DMA source of every padding chunk.
 __device__ __attribute__((aligned(256))) uint4 g_zero_page[16];
 
@@ -86,13 +93,19 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
   constexpr int FTH = NW * MS;
   constexpr int HWd = TW + KK - 1;
   constexpr int HROWS = (FTH + KK - 1) * HWd;
-  constexpr int NAI = (HROWS + 15) / 16;  // A DMA wave-instructions per stage (16 rows of 64 B each)
+  // A DMA wave-instructions per stage (16 rows of 64 B each).  With the
+  // BN/ReLU prologue the count is padded to a multiple of NW (every wave
+  // owns NAW chunks of the A region, the padding ones zero), so that each
+  // wave issues the same number of DMAs per stage: the late prologue below
+  // waits for its own A chunks with a compile-time vmcnt.
+  constexpr int NAI0 = (HROWS + 15) / 16;
+  constexpr int NAW = (NAI0 + NW - 1) / NW;
+  constexpr int NAI = PRO ? NAW * NW : NAI0;
   constexpr int TAPS = KK * KK;
   constexpr int NBI = TAPS * NT / 16;     // B DMA wave-instructions per stage
   constexpr int ABYTES = NAI * 1024;
   constexpr int BBYTES = NBI * 1024;
   constexpr int SLOT = ABYTES + BBYTES;
-  constexpr int NAW = (NAI + NW - 1) / NW;
   constexpr int NBW = (NBI + NW - 1) / NW;
   static_assert(NAW <= 16 && NBW <= 16, "per-wave DMA count");
   // transposed epilogue (H output): channel block CB and where its
@@ -149,7 +162,9 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
   int b_rel[NBW];
 #pragma unroll
   for (int k = 0; k < NBW; ++k) {
-    const int i = wave + NW * k;
+    // (PRO: a wave past the last B instruction repeats it -- the same bytes
+    // to the same place -- so every wave issues NBW B DMAs per stage)
+    const int i = PRO ? min(wave + NW * k, NBI - 1) : wave + NW * k;
     const int row = 16 * i + (lane >> 2);
     const int tap = row / NT, n = row - (row / NT) * NT;
     const int p = (lane & 3) ^ ((row >> 2) & 3);
@@ -207,6 +222,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
     const H* wsrc;
     uint32_t sbase;
     unsigned m;  // valid A chunks of this lane (bit k)
+    int c0;      // first input channel of the stage
+    int slot;
     bool on;
   };
   auto prep = [&](const Tile& tl, int s, int slot) __attribute__((always_inline)) {
@@ -237,6 +254,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
     d.xb = reinterpret_cast<const H*>(a.x.ptr) + xoff;
     d.wsrc = reinterpret_cast<const H*>(a.w) + ((int64_t)kdi * TAPS * a.cout_pad + tl.n0) * a.cin_pad + c0;
     d.sbase = lds_addr(lds) + slot * SLOT;
+    d.c0 = c0;
+    d.slot = slot;
     d.m = 0;
 #pragma unroll
     for (int k = 0; k < NAW; ++k) {
@@ -254,7 +273,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
         glds16(src, d.sbase + i * 1024);
       }
     } else if (q < NAW + NBW && !(a.ablate & 8)) {
-      const int i = wave + NW * (q - NAW);
+      const int i = PRO ? min(wave + NW * (q - NAW), NBI - 1) : wave + NW * (q - NAW);
       if (i < NBI) glds16(d.wsrc + b_rel[q - NAW], d.sbase + ABYTES + i * 1024);
     }
   };
@@ -294,6 +313,32 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
   // the groups so they interleave with the math.
   constexpr int ITERS = KK * 2;
   constexpr int QPG = (NQ + ITERS - 1) / ITERS;  // DMA instructions per group
+  // Late prologue (PRO): the BN-affine+ReLU transform of the NEXT stage's A
+  // chunks runs inside this stage's MFMA groups, from group TSTART on (one
+  // group after the last A DMA was issued), instead of between the DMA wait
+  // and the barrier where every wave of the workgroup did it at once.  It is
+  // branch-free: a lane's chunk outside the image stays zero, and in the
+  // last stage (no next stage) a chunk of the current slot is rewritten
+  // unchanged.  Measured: -2 % on the DUF 3x3x3 convs (the transform is
+  // issue-bound, ~26 VALU per 8 channels, not latency-bound).
+  constexpr int TSTART = ((NAW + QPG - 1) / QPG + 1 < ITERS) ? (NAW + QPG - 1) / QPG + 1 : ITERS - 1;
+  constexpr int NB_AFTER = (TSTART * QPG < NQ ? TSTART * QPG : NQ) - NAW;  // DMAs issued after the A chunks
+  // (1x1 convs: too few groups per stage -- their prologue stays up front)
+  constexpr bool LATE = PRO && NB_AFTER >= 0 && TSTART < ITERS;
+  const bool relu_in = (a.prologue & VSRK_PRO_RELU) != 0;
+  auto late_chunk = [&](const Dma& d, int k) __attribute__((always_inline)) {
+    const int sl = d.on ? d.slot : d.slot ^ 1;  // !on: d.slot is the other slot; rewrite the current one
+    uint4* p = reinterpret_cast<uint4*>(lds + sl * SLOT + (wave + NW * k) * 1024 + lane * 16);
+    const uint4 v = *p;
+    const uint4 t = prologue_lds<H>(v, d.c0 + a_p8[k], relu_in, lsc, lsh);
+    const bool ok = (d.m >> k) & 1;
+    uint4 o;
+    o.x = d.on ? (ok ? t.x : 0u) : v.x;
+    o.y = d.on ? (ok ? t.y : 0u) : v.y;
+    o.z = d.on ? (ok ? t.z : 0u) : v.z;
+    o.w = d.on ? (ok ? t.w : 0u) : v.w;
+    *p = o;
+  };
   // Software-pipelined by hand: group it+1's fragments are read before group
   // it's MFMAs and DMAs are issued (the DMA asm statements are memory
   // barriers to hipcc, which would otherwise never hoist a ds_read across
@@ -322,6 +367,14 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
     for (int it = 0; it < ITERS; ++it) {
       if (it + 1 < ITERS) load(fr[(it + 1) & 1], it + 1);
       const Frags& f = fr[it & 1];
+      if constexpr (LATE) {
+        if (it == TSTART) wait_vmcnt<(NB_AFTER >= 0 ? NB_AFTER : 0)>();
+        if (it >= TSTART) {
+#pragma unroll
+          for (int k = 0; k < NAW; ++k)
+            if (TSTART + (k * (ITERS - TSTART)) / NAW == it) late_chunk(d, k);
+        }
+      }
 #pragma unroll
       for (int kh = 0; kh < KK; ++kh)
 #pragma unroll
@@ -595,6 +648,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
   bool pend = false;
   int s = 0, slot = 0;
   unsigned mcur = issue(cur, 0, 0), mnxt = 0;
+  bool pro_done = false;  // stage s's A chunks were transformed by the previous compute (late prologue)
   __syncthreads();  // bias / prologue tables visible
   while (true) {
     // the stage after this one (possibly the first stage of the next tile)
@@ -608,7 +662,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of stage s has landed
     if constexpr (PRO) {
-      if (a.prologue) transform(slot, s, mcur);
+      if (!pro_done) transform(slot, s, mcur);  // first stage: no earlier compute transformed it
     }
     __syncthreads();  // every wave's DMA of stage s landed (and transformed); slot^1 is free
     if (pend) {
@@ -622,6 +676,9 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
     }
     Dma dn;
     dn.on = false;
+    dn.slot = slot ^ 1;
+    dn.m = 0;
+    dn.c0 = 0;
     if (have_next && !(a.ablate & 1)) {
       dn = prep(nxt, ns_, slot ^ 1);
       mnxt = dn.m;
@@ -629,6 +686,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
     if (pmode && s + 1 >= cur.nst) prefetch(cur);  // lands under this stage's MFMAs
     if (!(a.ablate & 2)) {
       compute(slot, dn);
+      pro_done = LATE && dn.on;
     } else if (dn.on) {
 #pragma unroll
       for (int q = 0; q < NQ; ++q) dma(dn, q);
@@ -655,7 +713,8 @@ template <int KK, int NT, int MS, int XS, int YS, int PRO, typename YT, int NW, 
 int launch_fast(FastArgs a, hipStream_t s) {
   constexpr int FTH = NW * MS;
   constexpr int HWd = TW + KK - 1;
-  constexpr int NAI = ((FTH + KK - 1) * HWd + 15) / 16;
+  constexpr int NAI0 = ((FTH + KK - 1) * HWd + 15) / 16;
+  constexpr int NAI = PRO ? (NAI0 + NW - 1) / NW * NW : NAI0;  // as in the kernel
   constexpr int SLOT = NAI * 1024 + KK * KK * NT * 64;
   constexpr bool TRANS = sizeof(YT) == 2;
   constexpr int CB = (!YS && SLOT >= NW * 32 * (NT * 4 + 16)) ? NT : 32;
