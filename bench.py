@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Throughput benchmark of the cardiac cine-MRI SR train step on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--models edsr,duf]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--models edsr,duf] [--config cfg2|cfg3|cfg5]
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver, N > 1)
 
 With --gpus N > 1 and no torchrun environment, bench.py starts the N ranks
@@ -28,6 +28,12 @@ roofline: the model's dominant conv, forward + data gradient + weight
           (HIP events on the launch stream, inside the timed region), against
           the dense MFMA peak of the compute dtype.  EDSR: the 33 body convs
           3x3 64->64; DUF: the six Conv3d 3x3x3 F->32 (F = 64..224).
+--config picks the BASELINE.json workload: cfg2 (default: ACDC, 4 x 16 x
+128 x 128 per GPU, bf16, EDSR + DUF), cfg3 (DSB15, DRF on 4 x 30-frame
+stacks), cfg5 (ACDC + DSB15 mixed, fp16, batch 8 per GPU, EDSR + DUF).
+measured_peak: this device's dense bf16 MFMA rate and HBM copy rate from
+          two microbenchmarks (vsrk_peak_mfma / vsrk_peak_copy), with each
+          roofline's fraction of the measured MFMA rate beside the vendor one.
 cpu_baseline: the CPU fp32 restatement of the same generator (oracle/,
           the reference's algorithm) timed on this host for a bounded sample
           (rank 0, N = 1 only), threads = the CPU share of this process.
@@ -57,6 +63,17 @@ from vsr_amd.losses import L1Loss  # noqa: E402
 METRIC = "voxels/sec fwd+bwd, 4× SR on 16×128×128 cine volumes, 1/2/4/8 MI355X"
 PEAK = {"bf16": 2.5e15, "fp16": 2.5e15, "fp32": 157.3e12}
 B, T, H, W, R = 4, 16, 128, 128, 4
+DATASET = "acdc"  # synthetic-data normalisation: "acdc", "dsb15" or "mixed" (half the volumes each)
+# BASELINE.json configs measurable on one node (--config): the batch / frames /
+# dataset / precision / models of each; cfg 2 is the default bench line.
+CONFIGS = {
+    "cfg2": dict(B=4, T=16, dataset="acdc", precision="bf16", models="edsr,duf",
+                 desc="ACDC 4x SR, 3D 16x128x128 volumes bf16, batch 4 per GPU"),
+    "cfg3": dict(B=4, T=30, dataset="dsb15", precision="bf16", models="drf",
+                 desc="DSB15 cine 4x SR, T=30 2D+t stacks (DRF), batch 4 per GPU"),
+    "cfg5": dict(B=8, T=16, dataset="mixed", precision="fp16", models="edsr,duf",
+                 desc="mixed ACDC+DSB15 4x SR, fp16 MFMA path, batch 8 per GPU"),
+}
 
 MODELS = {
     "edsr": dict(cls="EDSRNet", task="sisr",
@@ -205,7 +222,12 @@ def run_model(name, args, world, rank, dev):
     if world > 1:
         sync = GradSync(net, world)
         enable_sync_bn(net)  # DUF's BatchNorm3d: global-batch statistics (SyncBN)
-    lr, hr = synth_cine(B, T, H, W, R, seed=1234 + rank, device=dev)
+    if DATASET == "mixed":  # ConcatDataset of the two: per-sample normalisation constants
+        la, ha = synth_cine(B - B // 2, T, H, W, R, "acdc", seed=1234 + rank, device=dev)
+        lb, hb = synth_cine(B // 2, T, H, W, R, "dsb15", seed=4321 + rank, device=dev)
+        lr, hr = torch.cat([la, lb]), torch.cat([ha, hb])
+    else:
+        lr, hr = synth_cine(B, T, H, W, R, DATASET, seed=1234 + rank, device=dev)
     x, y = make_batch(spec["task"], lr, hr)
     l1 = L1Loss()
 
@@ -249,7 +271,7 @@ def run_model(name, args, world, rank, dev):
     res = {
         "value": world * vox_step * args.steps / elapsed, "unit": "voxels/s",
         "ms_per_step": elapsed / args.steps * 1e3,
-        "config": {"workload": f"cfg2: ACDC 4x SR, {B}x{T}x{H}x{W} LR cine volume per GPU, "
+        "config": {"workload": f"{args.config}: {CONFIGS[args.config]['desc']}; {B}x{T}x{H}x{W} LR voxels per GPU, "
                                f"{spec['cls']} ({spec['task'].upper()}), L1 + Adam",
                    "model": spec["cls"], "global_batch": world * B * T, "seq_len": T,
                    "parallelism": f"dp{world}" + ("+syncbn" if world > 1 and name == "duf" else "")},
@@ -292,6 +314,14 @@ def worker(args, world, rank, local):
             "config": first["config"], "roofline": first["roofline"], "final_loss": first["final_loss"],
             "models": results,
         }
+        if not args.no_peaks:
+            # the measured ceilings beside the vendor peak the fractions use
+            pk = F.measured_peaks(dev)
+            out["measured_peak"] = pk
+            for m in names:
+                rf = results[m]["roofline"]
+                if rf["achieved"]:
+                    rf["frac_of_measured_peak"] = rf["achieved"] / pk["mfma_bf16_tflops"]
         if world == 1 and not args.no_cpu_baseline:
             for m in names:
                 results[m]["cpu_baseline"] = cpu_baseline(m)
@@ -301,7 +331,16 @@ def worker(args, world, rank, local):
         dist.destroy_process_group()
 
 
+def apply_config(args):
+    """Set the module-level workload of --config (also in spawned ranks, which
+    re-import this module with the cfg-2 defaults)."""
+    global B, T, DATASET
+    cfg = CONFIGS[args.config]
+    B, T, DATASET = cfg["B"], cfg["T"], cfg["dataset"]
+
+
 def _spawned(local, args, world, port):
+    apply_config(args)
     os.environ.update(RANK=str(local), LOCAL_RANK=str(local), WORLD_SIZE=str(world),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     worker(args, world, local, local)
@@ -318,14 +357,19 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--models", default=os.environ.get("VSR_BENCH_MODELS", "edsr,duf"),
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS),
+                    help="BASELINE.json config (batch, frames, dataset, precision, default models)")
+    ap.add_argument("--models", default=os.environ.get("VSR_BENCH_MODELS"),
                     help="comma-separated subset of " + ",".join(MODELS))
     ap.add_argument("--model", default=None, help="a single model (same as --models NAME)")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--precision", default=None, choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-peaks", action="store_true", help="skip the measured MFMA / HBM peak microbenchmarks")
     args = ap.parse_args()
-    if args.model:
-        args.models = args.model
+    cfg = CONFIGS[args.config]
+    args.models = args.model or args.models or cfg["models"]
+    args.precision = args.precision or cfg["precision"]
+    apply_config(args)
     for m in args.models.split(","):
         if m not in MODELS:
             ap.error(f"unknown model {m!r}")

@@ -304,6 +304,16 @@ const char* vsrk_version(void);
 int vsrk_resize_bicubic(const double* src, int32_t n, int32_t ih, int32_t iw, int32_t oh, int32_t ow, double* dst,
                         int32_t round_clip, void* stream);
 
+/* Measured device peaks (the roofline fractions are quoted
+ * against the vendor peak; these give the measured ceiling beside it).
+ *   vsrk_peak_mfma: vsrk_peak_mfma_blocks() workgroups of 4 waves, each wave
+ *     iters x 4 v_mfma_f32_32x32x16_bf16 (32768 FLOP each) on register
+ *     operands; out: blocks * 256 floats (keeps the loop live).
+ *   vsrk_peak_copy: dst = src, 16-byte vectors, `bytes` a multiple of 16. */
+int32_t vsrk_peak_mfma_blocks(void);
+int vsrk_peak_mfma(int32_t iters, float* out, void* stream);
+int vsrk_peak_copy(const void* src, void* dst, int64_t bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

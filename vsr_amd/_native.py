@@ -72,6 +72,10 @@ _SIGS = {
     "vsrk_bn_workspace_size": (C.c_size_t, [C.c_int32]),
     "vsrk_bn_stats": (C.c_int, [_T5, _P, _P, _P, C.c_size_t, _P]),
     "vsrk_bn_stats_grouped": (C.c_int, [_T5, C.c_int32, _P, _P, _P, C.c_size_t, _P]),
+    "vsrk_peak_mfma_blocks": (C.c_int32, []),
+    "vsrk_peak_mfma": (C.c_int, [C.c_int32, _P, _P]),
+    "vsrk_peak_copy": (C.c_int, [_P, _P, C.c_int64, _P]),
+    "vsrk_gather_windows": (C.c_int, [_P] + [C.c_int32] * 4 + [_P] + [C.c_int32] * 4 + [_P, _P]),
     "vsrk_bn_finalize": (C.c_int, [_P, _P, C.c_double, _P, _P, C.c_float, C.c_float, _P, _P, _P, _P, _P, _P,
                                    C.c_int32, _P]),
     "vsrk_bn_fold_running": (C.c_int, [_P, _P, _P, _P, C.c_float, _P, _P, _P, _P, C.c_int32, _P]),

@@ -26,7 +26,7 @@ def sources() -> list[Path]:
 
 def _digest() -> str:
     h = hashlib.sha256()
-    for p in sources() + sorted(CSRC.glob("*.h")) + [INCLUDE / "vsrk.h"]:
+    for p in sources() + sorted(CSRC.glob("*.h")) + sorted(INCLUDE.glob("*.h")):
         h.update(p.name.encode())
         h.update(p.read_bytes())
     h.update(" ".join(FLAGS).encode())

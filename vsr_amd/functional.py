@@ -463,3 +463,35 @@ def prelu_bwd(y: torch.Tensor, dy: torch.Tensor, a: torch.Tensor, dx: torch.Tens
                                C.byref(ov), da.data_ptr(), 1 if accumulate_da else 0, ws.data_ptr(), ws.numel(),
                                N.stream_ptr(y.device)), "prelu_bwd")
     return dx
+
+
+# ------------------------------------------------------------ device peaks --
+def measured_peaks(device, mfma_iters: int = 20000, copy_bytes: int = 1 << 31, reps: int = 10) -> dict:
+    """Measured ceilings of this device (vsrk_peak_mfma / vsrk_peak_copy):
+    dense bf16 MFMA TFLOP/s on register operands and HBM copy TB/s (read +
+    write bytes), each the best of `reps` timed launches after a warm-up."""
+    lib = _lib()
+    blocks = lib.vsrk_peak_mfma_blocks()
+    out = torch.empty(blocks * 256, dtype=torch.float32, device=device)
+    src = torch.empty(copy_bytes // 4, dtype=torch.float32, device=device).uniform_()
+    dst = torch.empty_like(src)
+    sp = N.stream_ptr(device)
+
+    def best(fn):
+        fn()
+        t = []
+        for _ in range(reps):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            fn()
+            e.record()
+            e.synchronize()
+            t.append(s.elapsed_time(e) * 1e-3)
+        return min(t)
+
+    t_mfma = best(lambda: N.check(lib.vsrk_peak_mfma(mfma_iters, out.data_ptr(), sp), "peak_mfma"))
+    t_copy = best(lambda: N.check(lib.vsrk_peak_copy(src.data_ptr(), dst.data_ptr(), copy_bytes, sp), "peak_copy"))
+    flop = blocks * 4 * mfma_iters * 4 * 32768.0
+    return {"mfma_bf16_tflops": flop / t_mfma / 1e12, "hbm_copy_tbs": 2.0 * copy_bytes / t_copy / 1e12,
+            "method": f"v_mfma_f32_32x32x16_bf16 x{mfma_iters * 4} per wave, {blocks} x 4 waves; "
+                      f"{copy_bytes >> 20} MiB device copy (read+write); best of {reps}"}
