@@ -68,11 +68,17 @@ class GradSync:
         b = self._bucket_of[id(p)]
         self._remaining[b] -= 1
         if self._remaining[b] == 0:
+            join = getattr(self.net, "_join_wgrad", None)
+            if join is not None:
+                join()  # the bucket's weight gradients may still run on the side stream
             self._launch(b)
 
     def finish(self) -> None:
         """Wait for every bucket (launching any not yet complete), average, and
         re-attach .grad views (zero_grad(set_to_none=True) may have dropped them)."""
+        join = getattr(self.net, "_join_wgrad", None)
+        if join is not None:
+            join()
         for b, h in enumerate(self._handles):
             if h is None:
                 self._launch(b)

@@ -24,7 +24,7 @@ __all__ = [
 
 LOSS_KINDS = {"L1Loss": 0, "MSELoss": 1, "HuberLoss": 2, "CharbonnierLoss": 3}
 
-_ws: dict[int, torch.Tensor] = {}
+_ws: dict[tuple[int, int], torch.Tensor] = {}
 
 
 class KernelTimer:
@@ -66,8 +66,11 @@ timer: KernelTimer | None = None
 
 
 def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
-    """A per-device scratch buffer (grown on demand, stream-ordered reuse)."""
-    key = device.index if device.index is not None else torch.cuda.current_device()
+    """A scratch buffer per (device, current stream): grown on demand, reused in
+    stream order (the nets run weight gradients on a second stream, which
+    gets its own)."""
+    dev = device.index if device.index is not None else torch.cuda.current_device()
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
     buf = _ws.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)

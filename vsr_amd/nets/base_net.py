@@ -8,6 +8,8 @@ every parameter gradient with the deterministic wgrad kernels.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -18,12 +20,26 @@ _COMPUTE_DTYPES = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp16": t
 class BaseNet(nn.Module):
     """Base of every vsr_amd generator (reference: base_net.py:5-13)."""
 
+    # Side-stream weight gradients (see _on_wgrad_stream), measured on one
+    # MI355X at cfg 2 / 3 (profiles/r2e_side_stream_ab.txt): DRF -4.5 %
+    # (its per-frame convs leave CUs idle), EDSR -2.3 % but every conv's own
+    # launch time (the roofline) stretched by the sharing, DUF 86 -> 255 ms
+    # (the persistent one-workgroup-per-CU conv grids stall behind resident
+    # wgrad workgroups).  On for DRF only.
+    _OVERLAP_WGRAD = False
+
     def __init__(self):
         super().__init__()
         self.compute_dtype = torch.bfloat16
         self._grad_sink = None  # vsr_amd.ddp.GradSync when data-parallel
         # fp16 loss scale: None = automatic (see _loss_scale), else a fixed float
         self.loss_scale = None
+        # weight gradients on a second stream, overlapped with the data-gradient
+        # chain: per net class (_OVERLAP_WGRAD), VSR_OVERLAP_WGRAD=0/1 overrides
+        env = os.environ.get("VSR_OVERLAP_WGRAD")
+        self.overlap_wgrad = self._OVERLAP_WGRAD if env is None else env != "0"
+        self._side = None
+        self._side_used = False
 
     # -- gradient plumbing used by the subclasses' backward passes ----------
     def _grad_buffer(self, p: torch.Tensor) -> torch.Tensor:
@@ -40,6 +56,39 @@ class BaseNet(nn.Module):
             self._grad_sink.ready(p)
         else:
             grads[id(p)] = g
+
+    # -- weight gradients on a side stream ----------------------------------
+    # A weight gradient is a leaf of the backward graph: nothing in the step
+    # reads it before the optimizer.  Launched on a second stream (after the
+    # producer of its output gradient on the caller's stream), it overlaps the
+    # data-gradient chain: an MFMA-bound wgrad beside an HBM-bound BN / PReLU
+    # pass, or beside a conv whose grid leaves CUs idle (DRF's per-frame
+    # 4 x 128 x 128 launches).  Same kernels, same per-stream order:
+    # results stay bitwise reproducible.
+    def _on_wgrad_stream(self, fn, *reads):
+        """Run fn (a weight-gradient launch) on the side stream after all work
+        queued so far on the current stream; `reads` are the tensors it reads
+        (kept alive for the allocator until the side stream is done)."""
+        if not self.overlap_wgrad:
+            return fn()
+        main = torch.cuda.current_stream()
+        if self._side is None or self._side.device != main.device:
+            self._side = torch.cuda.Stream(main.device)
+        self._side.wait_stream(main)
+        with torch.cuda.stream(self._side):
+            out = fn()
+        for t in reads:
+            t.record_stream(self._side)
+        self._side_used = True
+        return out
+
+    def _join_wgrad(self) -> None:
+        """Make the current stream wait for every side-stream weight gradient
+        (before a gradient is consumed, or before a buffer a weight gradient
+        reads is overwritten in place)."""
+        if self._side_used:
+            torch.cuda.current_stream().wait_stream(self._side)
+            self._side_used = False
 
     def set_precision(self, precision: str, loss_scale: float | None = None) -> "BaseNet":
         """'bf16' or 'fp16' (16-bit activations and data gradients, fp32 master
@@ -114,6 +163,7 @@ class _TapeFunction(torch.autograd.Function):
             grads = tuple(g * scale if g is not None else None for g in grads)
         net._grad_unscale = 1.0 / scale
         g = net._backward(ctx.tape, grads if len(grads) > 1 else grads[0])
+        net._join_wgrad()
         ctx.tape = None
         if scale != 1.0 and net._grad_sink is None:
             for t in g.values():

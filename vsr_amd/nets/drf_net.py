@@ -121,6 +121,7 @@ class _OutBlock(nn.Sequential):
 
 
 class _DRFBase(BaseNet):
+    _OVERLAP_WGRAD = True  # per-frame launches leave CUs idle: weight gradients fill them
     def __init__(self, in_channels, out_channels, num_features, num_groups, upscale_factor):
         super().__init__()
         self.in_channels = in_channels
@@ -284,21 +285,27 @@ class _DRFBase(BaseNet):
         def wgrad(conv, x, dy, ksz, pad, **kw):
             dw, acc = gbuf(conv.weight)
             db, _ = gbuf(conv.bias)
-            F.conv_wgrad(x, dy, ksz, pad, dw.view(*dw.shape[:2], 1, *dw.shape[2:]), db, accumulate=acc, **kw)
+            self._on_wgrad_stream(
+                lambda: F.conv_wgrad(x, dy, ksz, pad, dw.view(*dw.shape[:2], 1, *dw.shape[2:]), db, accumulate=acc,
+                                     **kw), x, dy)
 
         def sp_wgrad(conv, x, dy, transposed):
             k_, s_, p_ = k, s, p
             cop = s_ * s_ * f if transposed else f
             cip = f if transposed else s_ * s_ * f
-            dweq = torch.empty((cop, cip, 1, 3, 3), dtype=torch.float32, device=dev)
-            dbeq = torch.empty(cop, dtype=torch.float32, device=dev)
-            if transposed:
-                F.conv_wgrad(x, dy, K3, P1, dweq, dbeq, dy_shuffle=s_)
-            else:
-                F.conv_wgrad(x, dy, K3, P1, dweq, dbeq, x_shuffle=s_)
             dw, acc = gbuf(conv.weight)
             db, _ = gbuf(conv.bias)
-            F.subpixel_wgrad_fold(dweq, dbeq, dw, db, k_, s_, p_, transposed, accumulate=acc)
+
+            def run():  # on the side stream: the sub-pixel wgrad and its fold
+                dweq = torch.empty((cop, cip, 1, 3, 3), dtype=torch.float32, device=dev)
+                dbeq = torch.empty(cop, dtype=torch.float32, device=dev)
+                if transposed:
+                    F.conv_wgrad(x, dy, K3, P1, dweq, dbeq, dy_shuffle=s_)
+                else:
+                    F.conv_wgrad(x, dy, K3, P1, dweq, dbeq, x_shuffle=s_)
+                F.subpixel_wgrad_fold(dweq, dbeq, dw, db, k_, s_, p_, transposed, accumulate=acc)
+
+            self._on_wgrad_stream(run, x, dy)
 
         def prelu(y, dy, pr, out, dy2=None):
             da, acc = gbuf(pr.weight)

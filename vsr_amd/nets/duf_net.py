@@ -219,7 +219,7 @@ class DUFNet(BaseNet):
             dw = self._grad_buffer(conv.weight)
             db = self._grad_buffer(conv.bias)
             w5 = dw if dw.dim() == 5 else dw.view(*dw.shape[:2], 1, *dw.shape[2:])
-            F.conv_wgrad(x, dy, ksz, pad, w5, db, **kw)
+            self._on_wgrad_stream(lambda: F.conv_wgrad(x, dy, ksz, pad, w5, db, **kw), x, dy)
             self._grad_done(grads, conv.weight, dw)
             self._grad_done(grads, conv.bias, db)
 

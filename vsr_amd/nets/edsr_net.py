@@ -135,7 +135,8 @@ class EDSRNet(BaseNet):
         def wgrad(conv, x, dy, **kw):
             dw = self._grad_buffer(conv.weight)
             db = self._grad_buffer(conv.bias)
-            F.conv_wgrad(x, dy, K3, P1, dw.view(*dw.shape[:2], 1, *dw.shape[2:]), db, **kw)
+            self._on_wgrad_stream(
+                lambda: F.conv_wgrad(x, dy, K3, P1, dw.view(*dw.shape[:2], 1, *dw.shape[2:]), db, **kw), x, dy)
             self._grad_done(grads, conv.weight, dw)
             self._grad_done(grads, conv.bias, db)
 
@@ -167,7 +168,9 @@ class EDSRNet(BaseNet):
             dpre = dgrad(c2, gcur, torch.empty_like(t), out_scale=blk.res_scale, mask=t)
             wgrad(c1, xin, dpre)
             if i == 0:
-                # dL/dhead = block-0 input grad + global skip grad, accumulated in place
+                # dL/dhead = block-0 input grad + global skip grad, accumulated in
+                # place -- into d_body, which the body conv's weight gradient reads
+                self._join_wgrad()
                 gcur = dgrad(c1, dpre, d_body, residual=gcur, accumulate=True)
             else:
                 gcur = dgrad(c1, dpre, torch.empty_like(xin), residual=gcur)
