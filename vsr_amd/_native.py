@@ -76,6 +76,9 @@ _SIGS = {
     "vsrk_peak_mfma": (C.c_int, [C.c_int32, _P, _P]),
     "vsrk_peak_copy": (C.c_int, [_P, _P, C.c_int64, _P]),
     "vsrk_gather_windows": (C.c_int, [_P] + [C.c_int32] * 4 + [_P] + [C.c_int32] * 4 + [_P, _P]),
+    "vsrk_dcn_im2col": (C.c_int, [_P] * 6),
+    "vsrk_dcn_col2im": (C.c_int, [_P] * 6),
+    "vsrk_dcn_coord_grad": (C.c_int, [_P] * 8),
     "vsrk_bn_finalize": (C.c_int, [_P, _P, C.c_double, _P, _P, C.c_float, C.c_float, _P, _P, _P, _P, _P, _P,
                                    C.c_int32, _P]),
     "vsrk_bn_fold_running": (C.c_int, [_P, _P, _P, _P, C.c_float, _P, _P, _P, _P, C.c_int32, _P]),
