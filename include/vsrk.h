@@ -281,6 +281,22 @@ int vsrk_bn_relu_bwd_apply(const vsrk_tensor5* x, const vsrk_tensor5* dz, const 
                            const float* mean, const float* invstd, const float* gamma, const float* sum_dy,
                            const float* sum_dy_xhat, double count, const vsrk_tensor5* dx, int32_t accumulate,
                            void* stream);
+/* Several BN+ReLU backward applies into ONE output block in one pass (DUF's
+ * dense layer: every later unit's bn1 adds its input gradient to the same
+ * concat channels, duf_net.py:122-128).  x, dx: the block (N, D, H, W, C);
+ * contributor i: dz over depths [d0, d0 + dz.d) of the block and its BN's
+ * per-channel operands (pointers at the block's first channel), as in
+ * vsrk_bn_relu_bwd_apply.  dx [+]= sum_i apply_i: x and dx move once instead
+ * of once per contributor.  1 <= n <= VSRK_BN_MULTI_MAX. */
+#define VSRK_BN_MULTI_MAX 3
+typedef struct vsrk_bn_contrib {
+  vsrk_tensor5 dz;
+  int32_t d0;
+  const float *scale, *shift, *mean, *invstd, *gamma, *sum_dy, *sum_dy_xhat;
+  double count;
+} vsrk_bn_contrib;
+int vsrk_bn_relu_bwd_apply_multi(const vsrk_tensor5* x, const vsrk_tensor5* dx, int32_t accumulate, int32_t n,
+                                 const vsrk_bn_contrib* contribs, void* stream);
 
 /* DUF dynamic upsampling (duf_net.py:67-97), fused: softmax over the k*k taps
  * of per-pixel logits (n, h, w, k*k*r*r) fp32 (tap-major, as the reference's

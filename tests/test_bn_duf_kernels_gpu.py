@@ -112,3 +112,33 @@ def test_duf_dynfilter(dtype):
     dl, dr = F.duf_dynfilter_bwd(x.to(DEV), lg.to(DEV), gout.to(DEV), k, r, dtype)
     tol = {torch.float32: 1e-5, torch.float16: 2e-3}.get(dtype, 8e-3)
     assert _rel(dl, lg64.grad) <= tol and _rel(dr, res64.grad) <= tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("ncontrib", [1, 2, 3])
+def test_bn_apply_multi_equals_sequential_applies(dtype, ncontrib):
+    """vsrk_bn_relu_bwd_apply_multi (DUF's deferred bn1 input gradients) vs
+    the single-contributor apply run once per contributor: every
+    contributor's dz covers its own depth window of the block."""
+    g = torch.Generator().manual_seed(11 + ncontrib)
+    n, D, h, w, c, cb = 2, 7, 5, 9, 64, 32
+    buf = (torch.randn((n, D, h, w, c + 16), generator=g) * 1.3 + 0.2).to(DEV, dtype)
+    x = buf[..., 16:16 + cb]  # the block: a channel slice of a concat buffer
+    base = (torch.randn((n, D, h, w, cb), generator=g) * 0.1).to(DEV, dtype)
+    cs, seq = [], base.clone()
+    for i in range(ncontrib):
+        d0, d1 = [(0, 7), (1, 6), (2, 5)][i]
+        dz = torch.randn((n, d1 - d0, h, w, c), generator=g).to(DEV, dtype)[..., 8:8 + cb]
+        sc = (torch.rand(cb, generator=g) + 0.3).to(DEV)
+        sh = torch.randn(cb, generator=g).to(DEV)
+        mean, invstd = torch.randn(cb, generator=g).to(DEV), (torch.rand(cb, generator=g) + 0.5).to(DEV)
+        st = torch.stack([sc, sh, mean, invstd])
+        gamma = (torch.rand(cb, generator=g) + 0.5).to(DEV)
+        red = torch.randn((2, cb), generator=g).to(DEV)
+        cnt = float(n * (d1 - d0) * h * w)
+        cs.append((dz, d0, st, gamma, red, cnt))
+        F.bn_relu_bwd_apply(x[:, d0:d1], dz, st, gamma, red, cnt, seq[:, d0:d1], True)
+    out = base.clone()
+    F.bn_relu_bwd_apply_multi(x, out, True, cs)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert (out.float() - seq.float()).abs().max().item() <= tol * max(1.0, seq.float().abs().max().item())

@@ -48,6 +48,16 @@ class ConvDesc(C.Structure):
     ]
 
 
+class BnContrib(C.Structure):
+    """vsrk_bn_contrib (include/vsrk.h)."""
+    _fields_ = [
+        ("dz", Tensor5), ("d0", C.c_int32),
+        ("scale", C.c_void_p), ("shift", C.c_void_p), ("mean", C.c_void_p), ("invstd", C.c_void_p),
+        ("gamma", C.c_void_p), ("sum_dy", C.c_void_p), ("sum_dy_xhat", C.c_void_p),
+        ("count", C.c_double),
+    ]
+
+
 # name -> (restype, argtypes)
 _P = C.c_void_p
 _T5 = C.POINTER(Tensor5)
@@ -85,6 +95,7 @@ _SIGS = {
     "vsrk_bn_apply": (C.c_int, [_T5, _P, _P, C.c_int32, _T5, _P]),
     "vsrk_bn_relu_bwd_reduce": (C.c_int, [_T5, _T5, _P, _P, _P, _P, _P, _P, _P, C.c_size_t, _P]),
     "vsrk_bn_relu_bwd_apply": (C.c_int, [_T5, _T5, _P, _P, _P, _P, _P, _P, _P, C.c_double, _T5, C.c_int32, _P]),
+    "vsrk_bn_relu_bwd_apply_multi": (C.c_int, [_T5, _T5, C.c_int32, C.c_int32, C.POINTER(BnContrib), _P]),
     "vsrk_duf_dynfilter_fwd": (C.c_int, [_P, _P, _P] + [C.c_int32] * 5 + [_P, _P]),
     "vsrk_duf_dynfilter_bwd": (C.c_int, [_P, _P, _P] + [C.c_int32] * 5 + [_P, _P, C.c_int32, _P]),
     "vsrk_conv_set_algo": (C.c_int, [C.c_int32]),

@@ -303,6 +303,132 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(View x, View dz,
   }
 }
 
+// NC contributors' BN+ReLU backward applies into one output block (see
+// vsrk_bn_relu_bwd_apply_multi): the same row walk and per-thread constants
+// as bn_relu_bwd_apply_kernel, x and dx moved once, each contributor's dz
+// read on the rows (depths) it covers.
+struct ContribDev {
+  View dz;
+  int d0, d1;
+  const float *scale, *shift, *mean, *invstd, *gamma, *sdy, *sdyx;
+  float inv_count;
+};
+template <int NC>
+struct ContribPack {
+  ContribDev c[NC];
+};
+
+template <typename T, int NC>
+__global__ __launch_bounds__(256) void bn_relu_bwd_apply_multi_kernel(View x, View dx, ContribPack<NC> cp, int nrows,
+                                                                      int accumulate) {
+  constexpr int E = Chunk<T>::E;
+  const int C = x.c;
+  const int cpv = (C + E - 1) / E;
+  const int vpb = blockDim.x / cpv;
+  const int ch = threadIdx.x % cpv, vl = threadIdx.x / cpv;
+  if (vl >= vpb) return;
+  const int c0 = ch * E;
+  const bool full = c0 + E <= C;
+  float sc[NC][E], sh[NC][E], k1[NC][E], k2[NC][E], k3[NC][E];
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const ContribDev& q = cp.c[i];
+      const int c = min(c0 + e, C - 1);
+      const float is = q.invstd[c], gm = q.gamma ? q.gamma[c] : 1.f;
+      const float a = gm * is, b = is * q.sdyx[c] * q.inv_count;
+      sc[i][e] = q.scale[c];
+      sh[i][e] = q.shift[c];
+      k1[i][e] = a;
+      k2[i][e] = -a * b;
+      k3[i][e] = a * (q.mean[c] * b - q.sdy[c] * q.inv_count);
+    }
+  for (int r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const int h = r % x.h, t = r / x.h, d = t % x.d, n = t / x.d;
+    const T* xr = reinterpret_cast<const T*>(x.ptr) + row_off(x, r) + c0;
+    T* orow = reinterpret_cast<T*>(dx.ptr) + row_off(dx, r) + c0;
+    const T* gr[NC];
+    bool on[NC];
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const ContribDev& q = cp.c[i];
+      on[i] = d >= q.d0 && d < q.d1;
+      gr[i] = reinterpret_cast<const T*>(q.dz.ptr) +
+              (n * q.dz.sn + (int64_t)(on[i] ? d - q.d0 : 0) * q.dz.sd + (int64_t)h * q.dz.sh) + c0;
+    }
+    // U voxels per pass with every load (x, dx, each active dz) issued before
+    // any is used; a scalar path for a partial last chunk
+    constexpr int U = 2;
+    for (int wb = vl; wb < x.w; wb += U * vpb) {
+      uint4 rx[U], ro[U], rg[NC][U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int w = wb + u * vpb;
+        const bool ok = full && w < x.w;
+        rx[u] = ok ? *reinterpret_cast<const uint4*>(xr + (int64_t)w * x.sw) : make_uint4(0, 0, 0, 0);
+        ro[u] = (ok && accumulate) ? *reinterpret_cast<const uint4*>(orow + (int64_t)w * dx.sw)
+                                   : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < NC; ++i)
+          rg[i][u] = (ok && on[i]) ? *reinterpret_cast<const uint4*>(gr[i] + (int64_t)w * cp.c[i].dz.sw)
+                                   : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int w = wb + u * vpb;
+        if (w >= x.w) break;
+        float f[E], o[E], g[NC][E];
+        if (full) {
+          Chunk<T>::unpack(rx[u], f);
+          Chunk<T>::unpack(ro[u], o);
+#pragma unroll
+          for (int i = 0; i < NC; ++i) Chunk<T>::unpack(rg[i][u], g[i]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const bool ok = c0 + e < C;
+            f[e] = ok ? to_f32<T>(xr[(int64_t)w * x.sw + e]) : 0.f;
+            o[e] = (ok && accumulate) ? to_f32<T>(orow[(int64_t)w * dx.sw + e]) : 0.f;
+#pragma unroll
+            for (int i = 0; i < NC; ++i)
+              g[i][e] = (ok && on[i]) ? to_f32<T>(gr[i][(int64_t)w * cp.c[i].dz.sw + e]) : 0.f;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+          if (!on[i]) continue;  // uniform per row
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const float dy = fmaf(f[e], sc[i][e], sh[i][e]) > 0.f ? g[i][e] : 0.f;
+            o[e] += fmaf(k1[i][e], dy, fmaf(k2[i][e], f[e], k3[i][e]));
+          }
+        }
+        T* po = orow + (int64_t)w * dx.sw;
+        if (full) {
+          *reinterpret_cast<uint4*>(po) = Chunk<T>::pack(o);
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e)
+            if (c0 + e < C) po[e] = from_f32<T>(o[e]);
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int NC>
+void launch_apply_multi(const vsrk_tensor5* x, const vsrk_tensor5* dx, int accumulate, const vsrk_bn_contrib* cs,
+                        int grid, int thr, int nrows, hipStream_t s) {
+  ContribPack<NC> cp;
+  for (int i = 0; i < NC; ++i) {
+    const vsrk_bn_contrib& q = cs[i];
+    cp.c[i] = ContribDev{make_view(&q.dz), q.d0, q.d0 + q.dz.d, q.scale, q.shift, q.mean, q.invstd, q.gamma,
+                         q.sum_dy, q.sum_dy_xhat, (float)(1.0 / q.count)};
+  }
+  bn_relu_bwd_apply_multi_kernel<T, NC><<<grid, thr, 0, s>>>(make_view(x), make_view(dx), cp, nrows, accumulate);
+}
+
 // y = x * scale + shift [relu] per channel (the standalone BatchNorm3d forward
 // of the op-level modules; the generators fold it into the next conv instead)
 template <typename T>
@@ -475,6 +601,43 @@ extern "C" int vsrk_bn_relu_bwd_apply(const vsrk_tensor5* x, const vsrk_tensor5*
                                                          mean, invstd, gamma, sum_dy, sum_dy_xhat,
                                                          (float)(1.0 / count), nrows, accumulate);
   VSRK_LAUNCH_CHECK("bn_relu_bwd_apply");
+  return VSRK_OK;
+}
+
+extern "C" int vsrk_bn_relu_bwd_apply_multi(const vsrk_tensor5* x, const vsrk_tensor5* dx, int32_t accumulate,
+                                            int32_t n, const vsrk_bn_contrib* cs, void* stream) {
+  VSRK_CHECK(x && dx && cs && n >= 1 && n <= VSRK_BN_MULTI_MAX, "bn_relu_bwd_apply_multi: bad argument");
+  VSRK_CHECK(x->dtype == dx->dtype && x->c == dx->c && x->n == dx->n && x->d == dx->d && x->h == dx->h &&
+                 x->w == dx->w && x->shuffle <= 1 && dx->shuffle <= 1,
+             "bn_relu_bwd_apply_multi: x / dx mismatch");
+  for (int i = 0; i < n; ++i) {
+    const vsrk_bn_contrib& q = cs[i];
+    VSRK_CHECK(q.dz.ptr && q.scale && q.shift && q.mean && q.invstd && q.sum_dy && q.sum_dy_xhat && q.count > 0,
+               "bn_relu_bwd_apply_multi: contributor %d: null operand", i);
+    VSRK_CHECK(q.dz.dtype == x->dtype && q.dz.c == x->c && q.dz.n == x->n && q.dz.h == x->h && q.dz.w == x->w &&
+                   q.d0 >= 0 && q.d0 + q.dz.d <= x->d && q.dz.shuffle <= 1,
+               "bn_relu_bwd_apply_multi: contributor %d does not fit the block", i);
+  }
+  const int E = vsrk_is16(x->dtype) ? 8 : 4;
+  const int cpv = ceil_div(x->c, E);
+  VSRK_CHECK(cpv <= 256, "bn_relu_bwd_apply_multi: too many channels (%d)", x->c);
+  const int64_t nr64 = (int64_t)x->n * x->d * x->h;
+  VSRK_CHECK(nr64 < (1ll << 31), "bn_relu_bwd_apply_multi: too many rows");
+  const int nrows = (int)nr64;
+  if (nrows == 0) return VSRK_OK;
+  const int thr = cpv * (256 / cpv);
+  const int grid = std::min(nrows, 4096);
+  hipStream_t s = (hipStream_t)stream;
+  auto go = [&](auto tag) {
+    using T = decltype(tag);
+    if (n == 1) launch_apply_multi<T, 1>(x, dx, accumulate, cs, grid, thr, nrows, s);
+    else if (n == 2) launch_apply_multi<T, 2>(x, dx, accumulate, cs, grid, thr, nrows, s);
+    else launch_apply_multi<T, 3>(x, dx, accumulate, cs, grid, thr, nrows, s);
+  };
+  if (x->dtype == VSRK_BF16) go(bf16{});
+  else if (x->dtype == VSRK_F16) go(f16{});
+  else go(float{});
+  VSRK_LAUNCH_CHECK("bn_relu_bwd_apply_multi");
   return VSRK_OK;
 }
 

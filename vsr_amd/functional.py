@@ -328,6 +328,35 @@ def bn_stats_depth(x: torch.Tensor) -> torch.Tensor:
     return out.transpose(0, 1)
 
 
+BN_MULTI_MAX = 3  # VSRK_BN_MULTI_MAX
+
+
+def bn_relu_bwd_apply_multi(x: torch.Tensor, dx: torch.Tensor, accumulate: bool, contribs) -> torch.Tensor:
+    """dx [+]= sum of up to BN_MULTI_MAX BN+ReLU backward applies over one block
+    x (N, D, H, W, C): contribs = [(dz, d0, st, gamma, red, count), ...] with dz
+    covering the block's depths [d0, d0 + dz.shape[1]), st / gamma / red already
+    sliced to the block's channels (bn_finalize rows, BN weight, reduce sums)."""
+    lib = _lib()
+    if not 1 <= len(contribs) <= BN_MULTI_MAX:
+        raise ValueError(f"1..{BN_MULTI_MAX} contributors")
+    arr = (N.BnContrib * len(contribs))()
+    keep = []
+    for i, (dz, d0, st, gamma, red, count) in enumerate(contribs):
+        st = st.contiguous()
+        red = red.contiguous()
+        keep += [st, red]
+        arr[i] = N.BnContrib(N.t5(dz), int(d0), st[0].data_ptr(), st[1].data_ptr(), st[2].data_ptr(),
+                             st[3].data_ptr(), N.ptr(gamma.contiguous() if gamma is not None else None),
+                             red[0].data_ptr(), red[1].data_ptr(), float(count))
+        if gamma is not None:
+            keep.append(gamma.contiguous())
+            arr[i].gamma = keep[-1].data_ptr()
+    xv, ov = N.t5(x), N.t5(dx)
+    N.check(lib.vsrk_bn_relu_bwd_apply_multi(C.byref(xv), C.byref(ov), 1 if accumulate else 0, len(contribs), arr,
+                                             N.stream_ptr(x.device)), "bn_relu_bwd_apply_multi")
+    return dx
+
+
 def bn_finalize(sums: torch.Tensor, count: float, gamma, beta, eps: float, momentum: float,
                 running_mean=None, running_var=None) -> torch.Tensor:
     """-> (4, C) fp32: scale, shift, mean, invstd (running stats updated in place)."""

@@ -118,6 +118,12 @@ class DUFNet(BaseNet):
         return st
 
     def _bn_backward(self, bn, x, dz, st, dx, accumulate, grads):
+        red = self._bn_backward_reduce(bn, x, dz, st, grads)
+        F.bn_relu_bwd_apply(x, dz, st, bn.weight, red, st.count, dx, accumulate)
+
+    def _bn_backward_reduce(self, bn, x, dz, st, grads):
+        """The reduce half of the BN+ReLU backward: writes dgamma / dbeta and
+        returns the (sum_dy, sum_dy_xhat) that feed the input gradient."""
         red = F.bn_relu_bwd_reduce(x, dz, st)
         # dgamma / dbeta are this rank's local sums: the data-parallel gradient
         # average (GradSync) combines them across ranks, as torch's
@@ -130,9 +136,9 @@ class DUFNet(BaseNet):
         if self.bn_allreduce is not None and st.count != float("inf"):
             red = red.clone()
             self.bn_allreduce(red)
-        F.bn_relu_bwd_apply(x, dz, st, bn.weight, red, st.count, dx, accumulate)
         self._grad_done(grads, bn.weight, gw)
         self._grad_done(grads, bn.bias, gb)
+        return red
 
     # ----------------------------------------------------------------------
     def _run(self, inputs, tape: dict | None):
@@ -251,10 +257,26 @@ class DUFNet(BaseNet):
         dzt = dgrad(dl.tail.conv, dfeat, torch.empty_like(Rt), (1, 3, 3), (0, 1, 1))
         dC = torch.zeros_like(C)
         self._bn_backward(dl.tail.bn, Rt, dzt, stt, dC[:, lo:hi, :, :, :ctot], True, grads)
+        # Each unit's bn1 input gradient lands in every concat channel below
+        # its f.  Instead of a read-modify-write of dC[..., :f] per unit, the
+        # units' (dz1, statistics) are kept and a channel block is summed in
+        # one pass over x / dC (up to F.BN_MULTI_MAX contributors per pass)
+        # right before the unit that needs it -- the head block at the end.
+        pending = []  # (lo, hi, f, dz1, st1, gamma, red, count) of the units done so far
+
+        def flush(dlo, dhi, c0, c1):
+            xs, out = C[:, dlo:dhi, :, :, c0:c1], dC[:, dlo:dhi, :, :, c0:c1]
+            cs = [(dz[..., c0:c1], plo - dlo, st[:, c0:c1], gm[c0:c1] if gm is not None else None, red[:, c0:c1], cnt)
+                  for plo, phi, pf, dz, st, gm, red, cnt in pending]
+            for j in range(0, len(cs), F.BN_MULTI_MAX):
+                F.bn_relu_bwd_apply_multi(xs, out, True, cs[j:j + F.BN_MULTI_MAX])
+
         for i in range(dl.n_units - 1, -1, -1):
             u = getattr(dl, f"conv{i}")
             lo, hi, olo, ohi, f, pad, st1, st2, t1 = tape["units"][i]
             R = C[:, lo:hi, :, :, :f]
+            if pending:
+                flush(olo, ohi, f, f + g)
             dx_i = dC[:, olo:ohi, :, :, f:f + g]
             wgrad(u.conv2, t1, dx_i, (3, 3, 3), pad, prologue=ARF, pro_scale=st2[0], pro_shift=st2[1])
             dz2 = dgrad(u.conv2, dx_i, torch.empty_like(t1), (3, 3, 3), pad)
@@ -262,7 +284,9 @@ class DUFNet(BaseNet):
             self._bn_backward(u.bn2, t1, dz2, st2, dt1, False, grads)
             wgrad(u.conv1, R, dt1, K1, P0, prologue=ARF, pro_scale=st1[0], pro_shift=st1[1])
             dz1 = dgrad(u.conv1, dt1, dz2, K1, P0)  # dz2 is dead: reuse its storage
-            self._bn_backward(u.bn1, R, dz1, st1, dC[:, lo:hi, :, :, :f], True, grads)
+            red1 = self._bn_backward_reduce(u.bn1, R, dz1, st1, grads)
+            pending.append((lo, hi, f, dz1, st1, u.bn1.weight, red1, st1.count))
+        flush(0, C.shape[1], 0, 64)
         wgrad(self.head, tape["xv"], dC[..., :64], (1, 3, 3), (0, 1, 1))
         return grads
 
