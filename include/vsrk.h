@@ -281,6 +281,20 @@ int vsrk_bn_relu_bwd_apply(const vsrk_tensor5* x, const vsrk_tensor5* dz, const 
                            const float* mean, const float* invstd, const float* gamma, const float* sum_dy,
                            const float* sum_dy_xhat, double count, const vsrk_tensor5* dx, int32_t accumulate,
                            void* stream);
+/* Every conv weight of a step repacked in ONE launch (the per-conv
+ * vsrk_conv_pack_weight launches were ~4 us each, 73 per EDSR step).
+ * descs: n records in DEVICE memory (built once by the caller and reused
+ * every step: the weights are updated in place by the optimizer); record i
+ * packs fp32 w (cout, cin, kd, kh, kw) into packed as vsrk_conv_pack_weight
+ * would (mode, perm_r); max_elems = the largest vsrk_conv_packed_elems. */
+typedef struct vsrk_pack_desc {
+  const float* w;
+  void* packed;
+  int32_t cout, cin, kd, kh, kw, mode, perm_r;
+  int32_t reserved;
+} vsrk_pack_desc;
+int vsrk_conv_pack_weights(int32_t dtype, int32_t n, const vsrk_pack_desc* descs, int64_t max_elems, void* stream);
+
 /* Several BN+ReLU backward applies into ONE output block in one pass (DUF's
  * dense layer: every later unit's bn1 adds its input gradient to the same
  * concat channels, duf_net.py:122-128).  x, dx: the block (N, D, H, W, C);

@@ -58,6 +58,13 @@ class BnContrib(C.Structure):
     ]
 
 
+class PackDesc(C.Structure):
+    """vsrk_pack_desc (include/vsrk.h)."""
+    _fields_ = [("w", C.c_void_p), ("packed", C.c_void_p),
+                ("cout", C.c_int32), ("cin", C.c_int32), ("kd", C.c_int32), ("kh", C.c_int32), ("kw", C.c_int32),
+                ("mode", C.c_int32), ("perm_r", C.c_int32), ("reserved", C.c_int32)]
+
+
 # name -> (restype, argtypes)
 _P = C.c_void_p
 _T5 = C.POINTER(Tensor5)
@@ -65,6 +72,7 @@ _CD = C.POINTER(ConvDesc)
 _SIGS = {
     "vsrk_conv_packed_elems": (C.c_size_t, [C.c_int32] * 6),
     "vsrk_conv_pack_weight": (C.c_int, [C.c_int32, _P] + [C.c_int32] * 7 + [_P, _P]),
+    "vsrk_conv_pack_weights": (C.c_int, [C.c_int32, C.c_int32, _P, C.c_int64, _P]),
     "vsrk_conv_fwd": (C.c_int, [_CD, _T5, _P, _P, _P, _P, _T5, _T5, _T5, _P]),
     "vsrk_conv_wgrad_workspace_size": (C.c_size_t, [_CD, _T5, _T5]),
     "vsrk_conv_wgrad": (C.c_int, [_CD, _T5, _T5, _P, _P, C.c_float, C.c_int32, _P, _P, C.c_int32, _P,

@@ -367,6 +367,39 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, T* __restrict__ 
   out[idx] = from_f32<T>(v);
 }
 
+// one launch for many weights: blockIdx.y = weight, grid-stride in x
+template <typename T>
+__global__ void pack_weights_kernel(const vsrk_pack_desc* __restrict__ descs) {
+  const vsrk_pack_desc d = descs[blockIdx.y];
+  const int co_pad = round_up(d.mode == 0 ? d.cout : d.cin, 128), ci_pad = round_up(d.mode == 0 ? d.cin : d.cout, 32);
+  const int64_t total = (int64_t)d.kd * d.kh * d.kw * co_pad * ci_pad;
+  T* out = reinterpret_cast<T*>(d.packed);
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * blockDim.x) {
+    const int i = idx % ci_pad;
+    const int64_t t1 = idx / ci_pad;
+    const int o = t1 % co_pad;
+    const int tap = t1 / co_pad;
+    const int kwi = tap % d.kw, khi = (tap / d.kw) % d.kh, kdi = tap / (d.kw * d.kh);
+    int co, ci, sd, sh, sw;
+    if (d.mode == 0) {
+      co = o; ci = i; sd = kdi; sh = khi; sw = kwi;
+    } else {
+      co = i; ci = o; sd = d.kd - 1 - kdi; sh = d.kh - 1 - khi; sw = d.kw - 1 - kwi;
+    }
+    float v = 0.f;
+    if (co < d.cout && ci < d.cin) {
+      int cot = co;
+      if (d.perm_r > 1) {
+        const int rr = d.perm_r * d.perm_r, cp = d.cout / rr;
+        const int sub = co / cp, cc = co - sub * cp;
+        cot = cc * rr + sub;
+      }
+      v = d.w[((((int64_t)cot * d.cin + ci) * d.kd + sd) * d.kh + sh) * d.kw + sw];
+    }
+    out[idx] = from_f32<T>(v);
+  }
+}
+
 }  // namespace
 extern "C" size_t vsrk_conv_packed_elems(int32_t cout, int32_t cin, int32_t kd, int32_t kh, int32_t kw,
                                          int32_t mode) {
@@ -396,6 +429,19 @@ extern "C" int vsrk_conv_pack_weight(int32_t dtype, const float* w, int32_t cout
     pack_weight_kernel<float><<<grid, blk, 0, s>>>(w, (float*)packed, cout, cin, kd, kh, kw, mode, perm_r,
                                                    co_pad, ci_pad, total);
   VSRK_LAUNCH_CHECK("conv_pack_weight");
+  return VSRK_OK;
+}
+
+extern "C" int vsrk_conv_pack_weights(int32_t dtype, int32_t n, const vsrk_pack_desc* descs, int64_t max_elems,
+                                      void* stream) {
+  VSRK_CHECK(descs && n >= 0 && n < 65536 && max_elems >= 0, "conv_pack_weights: bad argument");
+  if (n == 0 || max_elems == 0) return VSRK_OK;
+  const int gx = (int)std::min<int64_t>(ceil_div64(max_elems, 256), 256);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VSRK_BF16) pack_weights_kernel<bf16><<<dim3(gx, n), 256, 0, s>>>(descs);
+  else if (dtype == VSRK_F16) pack_weights_kernel<f16><<<dim3(gx, n), 256, 0, s>>>(descs);
+  else pack_weights_kernel<float><<<dim3(gx, n), 256, 0, s>>>(descs);
+  VSRK_LAUNCH_CHECK("conv_pack_weights");
   return VSRK_OK;
 }
 

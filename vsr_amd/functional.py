@@ -106,6 +106,46 @@ def pack_weight(w: torch.Tensor, mode: int, dtype: torch.dtype, perm_r: int = 1)
     return out
 
 
+class WeightPacker:
+    """All the packed conv weights of a step in one launch
+    (vsrk_conv_pack_weights).  specs: [(weight, mode, perm_r), ...] of fp32
+    torch conv weights; the packed buffers and the device descriptor table
+    are allocated once and reused every step (the optimizer updates the
+    weights in place; a moved weight rebuilds the table).  run() returns
+    {(id(weight), mode, perm_r): packed tensor}."""
+
+    def __init__(self, specs, dtype: torch.dtype):
+        self.specs = [(w, int(m), int(r)) for w, m, r in specs]
+        self.dtype = dtype
+        self._ptrs = None
+
+    def _build(self):
+        lib = _lib()
+        dev = self.specs[0][0].device
+        descs = (N.PackDesc * len(self.specs))()
+        self.out, self.max_elems = {}, 0
+        for i, (w, m, r) in enumerate(self.specs):
+            if w.dtype != torch.float32 or not w.is_contiguous():
+                raise ValueError("WeightPacker needs contiguous fp32 weights")
+            cout, cin = w.shape[:2]
+            kd, kh, kw = _kdims(w)
+            n = lib.vsrk_conv_packed_elems(cout, cin, kd, kh, kw, m)
+            buf = torch.empty(n, dtype=self.dtype, device=dev)
+            self.out[(id(w), m, r)] = buf
+            self.max_elems = max(self.max_elems, n)
+            descs[i] = N.PackDesc(w.data_ptr(), buf.data_ptr(), cout, cin, kd, kh, kw, m, r, 0)
+        raw = torch.frombuffer(bytearray(C.string_at(C.addressof(descs), C.sizeof(descs))), dtype=torch.uint8)
+        self.table = raw.to(dev)
+        self._ptrs = tuple(w.data_ptr() for w, _, _ in self.specs)
+
+    def run(self) -> dict:
+        if self._ptrs != tuple(w.data_ptr() for w, _, _ in self.specs):
+            self._build()
+        N.check(_lib().vsrk_conv_pack_weights(N.dtype_code(self.dtype), len(self.specs), self.table.data_ptr(),
+                                              self.max_elems, N.stream_ptr(self.table.device)), "conv_pack_weights")
+        return self.out
+
+
 def _desc(k, pad, prologue=PRO_NONE, act=ACT_NONE, out_scale=1.0, accumulate=False, bias_r=1,
           act_param=None, mask_slope=None) -> N.ConvDesc:
     kd, kh, kw = k

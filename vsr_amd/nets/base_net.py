@@ -13,6 +13,8 @@ import os
 import torch
 import torch.nn as nn
 
+from .. import functional as F
+
 _COMPUTE_DTYPES = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp16": torch.float16,
                    "float16": torch.float16, "fp32": torch.float32, "float32": torch.float32}
 
@@ -40,6 +42,7 @@ class BaseNet(nn.Module):
         self.overlap_wgrad = self._OVERLAP_WGRAD if env is None else env != "0"
         self._side = None
         self._side_used = False
+        self._packers: dict = {}
 
     # -- gradient plumbing used by the subclasses' backward passes ----------
     def _grad_buffer(self, p: torch.Tensor) -> torch.Tensor:
@@ -81,6 +84,16 @@ class BaseNet(nn.Module):
             t.record_stream(self._side)
         self._side_used = True
         return out
+
+    def _pack_weights(self, specs) -> dict:
+        """Pack every (weight, mode, perm_r) of specs in one launch (persistent
+        buffers, see functional.WeightPacker) -> {(id(weight), mode, perm_r): packed}."""
+        cd = self.compute_dtype
+        key = (cd, tuple((id(w), m, r) for w, m, r in specs))
+        pk = self._packers.get(key)
+        if pk is None:
+            pk = self._packers[key] = F.WeightPacker(specs, cd)
+        return pk.run()
 
     def _join_wgrad(self) -> None:
         """Make the current stream wait for every side-stream weight gradient

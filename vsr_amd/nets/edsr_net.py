@@ -91,32 +91,41 @@ class EDSRNet(BaseNet):
         new = lambda hh, ww, c: torch.empty((b, 1, hh, ww, c), dtype=cd, device=dev)  # noqa: E731
         xv = F.to_view(x, cd, cpad=8)[..., :cin]  # chunk-aligned storage for the 1-channel input
         head = self.head[0]
-        h0 = F.conv(xv, F.pack_weight(head.weight, 0, cd), new(h, w, f), K3, P1, bias=head.bias)
+        specs = [(head.weight, 0, 1)] + [(c.weight, 0, 1) for blk in self._blocks()
+                                         for c in (blk.body.conv1, blk.body.conv2)]
+        specs += [(self.body.conv.weight, 0, 1)] + [(c.weight, 0, s) for c, s in self._ups()]
+        specs += [(self.tail.conv.weight, 0, 1)]
+        pk = self._pack_weights(specs)  # every forward weight in one launch
+
+        def P(conv, perm=1):
+            return pk[(id(conv.weight), 0, perm)]
+
+        h0 = F.conv(xv, P(head), new(h, w, f), K3, P1, bias=head.bias)
         saved = []
         cur = h0
         for blk in self._blocks():
             c1, c2 = blk.body.conv1, blk.body.conv2
-            t = F.conv(cur, F.pack_weight(c1.weight, 0, cd), new(h, w, f), K3, P1, bias=c1.bias, act=F.ACT_RELU)
-            nxt = F.conv(t, F.pack_weight(c2.weight, 0, cd), new(h, w, f), K3, P1, bias=c2.bias,
+            t = F.conv(cur, P(c1), new(h, w, f), K3, P1, bias=c1.bias, act=F.ACT_RELU)
+            nxt = F.conv(t, P(c2), new(h, w, f), K3, P1, bias=c2.bias,
                          out_scale=blk.res_scale, residual=cur)
             saved.append((cur, t))
             cur = nxt
         bc = self.body.conv
-        body_out = F.conv(cur, F.pack_weight(bc.weight, 0, cd), new(h, w, f), K3, P1, bias=bc.bias, residual=h0)
+        body_out = F.conv(cur, P(bc), new(h, w, f), K3, P1, bias=bc.bias, residual=h0)
         ups_in = []
         u, hh, ww = body_out, h, w
         for conv, s in self._ups():
             nxt = torch.empty((b, 1, hh * s, ww * s, f), dtype=cd, device=dev)
-            F.conv(u, F.pack_weight(conv.weight, 0, cd, perm_r=s), nxt, K3, P1, bias=conv.bias, y_shuffle=s)
+            F.conv(u, P(conv, s), nxt, K3, P1, bias=conv.bias, y_shuffle=s)
             ups_in.append(u)
             u, hh, ww = nxt, hh * s, ww * s
         tc = self.tail.conv
         y = torch.empty((b, self.out_channels, hh, ww), dtype=torch.float32, device=dev)
         yv = y.view(b, 1, hh, ww, 1) if self.out_channels == 1 else None
         if yv is not None:
-            F.conv(u, F.pack_weight(tc.weight, 0, cd), yv, K3, P1, bias=tc.bias)
+            F.conv(u, P(tc), yv, K3, P1, bias=tc.bias)
         else:
-            tmp = F.conv(u, F.pack_weight(tc.weight, 0, cd), torch.empty((b, 1, hh, ww, self.out_channels),
+            tmp = F.conv(u, P(tc), torch.empty((b, 1, hh, ww, self.out_channels),
                                                                          dtype=torch.float32, device=dev),
                          K3, P1, bias=tc.bias)
             y = F.from_view(tmp)
@@ -140,8 +149,13 @@ class EDSRNet(BaseNet):
             self._grad_done(grads, conv.weight, dw)
             self._grad_done(grads, conv.bias, db)
 
+        specs = [(self.tail.conv.weight, 1, 1)] + [(c.weight, 1, s) for c, s in self._ups()]
+        specs += [(self.body.conv.weight, 1, 1)] + [(c.weight, 1, 1) for blk in self._blocks()
+                                                    for c in (blk.body.conv1, blk.body.conv2)]
+        pk = self._pack_weights(specs)  # every data-gradient weight in one launch
+
         def dgrad(conv, dy, out, perm_r=1, **kw):
-            return F.conv(dy, F.pack_weight(conv.weight, 1, cd, perm_r=perm_r), out, K3, P1, **kw)
+            return F.conv(dy, pk[(id(conv.weight), 1, perm_r)], out, K3, P1, **kw)
 
         # tail conv
         u = tape["tail_in"]
