@@ -192,16 +192,35 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 1 : 2) void conv_fast_kernel(Fas
   struct Tile {
     int nb, dz, h0, w0, n0, kd_lo, nst;
   };
+  // Tile order: output channel tile fastest, then -- for a depth kernel
+  // (kd > 1) -- output depth, then columns, rows, sample.  With depth next,
+  // the workgroups of one XCD (a contiguous tile range) walk the depths of a
+  // few spatial tiles together, so each staged input slice serves its kd
+  // output depths out of that XCD's L2; in the (column, row, depth) order an
+  // XCD swept a whole 128 x 128 slice per depth and three F-channel input
+  // slices (6-21 MB) overflowed its 4 MB L2: the DUF 3x3x3 conv read 2.15x
+  // its algorithmic bytes from HBM (PMC, profiles/traffic_duf_bf16.json).
+  const bool depth_major = a.kd > 1;
   auto decode = [&](int t) __attribute__((always_inline)) {
     Tile tl;
     const int tn = t % a.ntn;
     int tm = t / a.ntn;
-    const int tw_i = tm % a.tiles_w;
-    tm /= a.tiles_w;
-    const int th_i = tm % a.tiles_h;
-    tm /= a.tiles_h;
-    tl.dz = tm % a.y.d;
-    tl.nb = tm / a.y.d;
+    int tw_i, th_i;
+    if (depth_major) {
+      tl.dz = tm % a.y.d;
+      tm /= a.y.d;
+      tw_i = tm % a.tiles_w;
+      tm /= a.tiles_w;
+      th_i = tm % a.tiles_h;
+      tl.nb = tm / a.tiles_h;
+    } else {
+      tw_i = tm % a.tiles_w;
+      tm /= a.tiles_w;
+      th_i = tm % a.tiles_h;
+      tm /= a.tiles_h;
+      tl.dz = tm % a.y.d;
+      tl.nb = tm / a.y.d;
+    }
     tl.h0 = th_i * FTH;
     tl.w0 = tw_i * TW;
     tl.n0 = tn * NT;
