@@ -255,28 +255,31 @@ class DUFNet(BaseNet):
         Rt = C[:, lo:hi, :, :, :ctot]
         wgrad(dl.tail.conv, Rt, dfeat, (1, 3, 3), (0, 1, 1), prologue=ARF, pro_scale=stt[0], pro_shift=stt[1])
         dzt = dgrad(dl.tail.conv, dfeat, torch.empty_like(Rt), (1, 3, 3), (0, 1, 1))
-        dC = torch.zeros_like(C)
-        self._bn_backward(dl.tail.bn, Rt, dzt, stt, dC[:, lo:hi, :, :, :ctot], True, grads)
+        # dC needs no zero fill: every block window is first written whole by
+        # its flush (accumulate off: rows no contributor covers become zero)
+        dC = torch.empty_like(C)
         # Each unit's bn1 input gradient lands in every concat channel below
         # its f.  Instead of a read-modify-write of dC[..., :f] per unit, the
         # units' (dz1, statistics) are kept and a channel block is summed in
         # one pass over x / dC (up to F.BN_MULTI_MAX contributors per pass)
         # right before the unit that needs it -- the head block at the end.
-        pending = []  # (lo, hi, f, dz1, st1, gamma, red, count) of the units done so far
+        # (lo, hi, f, dz, st, gamma, red, count) of the BNs done so far: the
+        # tail's bn over every channel at the last depth, then each unit's bn1
+        red_t = self._bn_backward_reduce(dl.tail.bn, Rt, dzt, stt, grads)
+        pending = [(lo, hi, ctot, dzt, stt, dl.tail.bn.weight, red_t, stt.count)]
 
         def flush(dlo, dhi, c0, c1):
             xs, out = C[:, dlo:dhi, :, :, c0:c1], dC[:, dlo:dhi, :, :, c0:c1]
             cs = [(dz[..., c0:c1], plo - dlo, st[:, c0:c1], gm[c0:c1] if gm is not None else None, red[:, c0:c1], cnt)
                   for plo, phi, pf, dz, st, gm, red, cnt in pending]
             for j in range(0, len(cs), F.BN_MULTI_MAX):
-                F.bn_relu_bwd_apply_multi(xs, out, True, cs[j:j + F.BN_MULTI_MAX])
+                F.bn_relu_bwd_apply_multi(xs, out, j > 0, cs[j:j + F.BN_MULTI_MAX])
 
         for i in range(dl.n_units - 1, -1, -1):
             u = getattr(dl, f"conv{i}")
             lo, hi, olo, ohi, f, pad, st1, st2, t1 = tape["units"][i]
             R = C[:, lo:hi, :, :, :f]
-            if pending:
-                flush(olo, ohi, f, f + g)
+            flush(olo, ohi, f, f + g)
             dx_i = dC[:, olo:ohi, :, :, f:f + g]
             wgrad(u.conv2, t1, dx_i, (3, 3, 3), pad, prologue=ARF, pro_scale=st2[0], pro_shift=st2[1])
             dz2 = dgrad(u.conv2, dx_i, torch.empty_like(t1), (3, 3, 3), pad)
