@@ -217,7 +217,8 @@ def run_model(name, args, world, rank, dev):
     spec = MODELS[name]
     torch.manual_seed(0)  # identical initial weights on every rank
     net = getattr(nets, spec["cls"])(**spec["kwargs"]).to(dev).set_precision(args.precision).train()
-    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
+    graph = args.graph and world == 1  # (collectives stay outside graphs)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4, capturable=graph)
     sync = None
     if world > 1:
         sync = GradSync(net, world)
@@ -244,21 +245,46 @@ def run_model(name, args, world, rank, dev):
         opt.step()
         return loss
 
-    for _ in range(args.warmup):
-        step()
     match, kdesc = dominant(name, args.precision)
-    F.timer = F.KernelTimer(match)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
+    if graph:
+        # --graph: the whole step (forward, loss, backward, Adam) captured into
+        # one HIP graph after eager warm-up on a side stream; the timed steps
+        # are replays.  The roofline kernels are timed on one eager step.
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(2, args.warmup)):
+                step()
+        torch.cuda.current_stream().wait_stream(side)
+        F.timer = F.KernelTimer(match)
+        step()
+        timer, F.timer = F.timer, None
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            g.replay()
+        torch.cuda.synchronize()
+        F.timer = timer
+        timer.steps = 1
+    else:
+        for _ in range(args.warmup):
+            step()
+        F.timer = F.KernelTimer(match)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            loss = step()
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     flop, kernel_s, launches = F.timer.totals()
+    tsteps = getattr(F.timer, "steps", args.steps)  # steps the kernel timer saw
     F.timer = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
@@ -278,9 +304,10 @@ def run_model(name, args, world, rank, dev):
         "roofline": {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None, "peak": peak / 1e12,
                      "unit": "TFLOP/s", "frac": achieved / peak if achieved else None, "traffic": traffic,
                      "traffic_kernel": tkern, "kernel": kdesc,
-                     "kernel_ms_per_step": kernel_s / args.steps * 1e3, "launches_per_step": launches / args.steps,
-                     "flop_per_step": flop / args.steps},
+                     "kernel_ms_per_step": kernel_s / tsteps * 1e3, "launches_per_step": launches / tsteps,
+                     "flop_per_step": flop / tsteps},
         "final_loss": float(loss.item()),
+        "graph": graph,
     }
     del net, opt, sync
     torch.cuda.empty_cache()
@@ -365,6 +392,8 @@ def main():
     ap.add_argument("--precision", default=None, choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured MFMA / HBM peak microbenchmarks")
+    ap.add_argument("--graph", action="store_true",
+                    help="time replays of the whole step captured into one HIP graph (N = 1)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     args.models = args.model or args.models or cfg["models"]
