@@ -131,6 +131,12 @@ int vsrk_conv_set_path(const char* path, int32_t mode);
  * over a different split, so they agree within fp32 rounding). */
 int vsrk_conv_set_grid_cap(int32_t max_workgroups);
 
+/* Test knob of the rolling-depth Conv3d 3x3x3 path (path "roll" of
+ * vsrk_conv_set_path: 16-bit forward / data gradient of DUF's dense-unit convs,
+ * duf_net.py:203,214): output depths per tile, 0 = automatic (as many as keep
+ * >= 2 tiles per CU).  Results are identical for every setting. */
+int vsrk_conv_set_roll_depth(int32_t depths);
+
 /* Weight/bias gradient (autograd of nn.Conv*d.weight/.bias in loss.backward(),
  * base_trainer.py:128).  dw is fp32 in torch layout (cout, cin, kd, kh, kw);
  * `perm_r` as in vsrk_conv_pack_weight.  Deterministic: per-workgroup fp32

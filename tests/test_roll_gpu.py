@@ -1,0 +1,139 @@
+"""Parity of the rolling-depth Conv3d 3x3x3 kernel (conv_roll.hip: the 16-bit
+forward of DUF's dense-unit convs, duf_net.py:203,214, and their input
+gradient) against torch fp64 on the CPU.
+
+The kernel walks the input depth slices of a tile once and keeps one
+accumulator bank per output depth in flight, so the cases cover what that
+walk can get wrong: depth padding 1 (pad-1 units), 0 (depth-valid units,
+down to one output depth) and 2 (the data gradient of a depth-valid unit),
+partial spatial tiles, output-channel tiles of 32 with a partial last one,
+channel-slice views of a wider buffer (the concat layout), the BN-affine+ReLU
+prologue, and tiles that cover only part of the depth range (the depth-run
+knob) or several tiles per workgroup (the grid cap).  Every depth-run / grid
+setting must give BITWISE the same output: the accumulation order of an
+output voxel does not depend on the tiling.
+
+Tolerances as tests/test_conv_kernels_gpu.py: inputs and weights rounded to
+the 16-bit type before the fp64 reference; max |d| <= 1.5e-2 * max|ref|
+(bf16), 2e-3 * max|ref| (fp16).
+"""
+import pytest
+import torch
+import torch.nn.functional as Fn
+
+from vsr_amd import functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _tol(dtype, ref):
+    scale = max(ref.abs().max().item(), 1e-3)
+    return (2e-3 if dtype == torch.float16 else 1.5e-2) * scale
+
+
+def _q(t, dtype):
+    return t.to(dtype).double()
+
+
+def _ref(x_cl, w, b, pad):
+    y = Fn.conv3d(x_cl.permute(0, 4, 1, 2, 3), w, b, padding=pad)
+    return y.permute(0, 2, 3, 4, 1)
+
+
+CASES = [
+    # (N, D, H, W, Cin, Cout, depth pad, channel offset in a wider buffer)
+    (2, 5, 9, 35, 32, 32, 1, 0),      # partial row / column tiles
+    (1, 7, 16, 32, 64, 32, 1, 8),     # DUF pad-1 unit shape (one full tile), sliced input
+    (1, 7, 12, 40, 48, 32, 0, 0),     # depth-valid unit: 7 -> 5
+    (2, 3, 17, 33, 16, 40, 0, 16),    # 3 -> 1 output depth, cout 40: a partial 32-channel tile
+    (1, 5, 10, 34, 32, 96, 2, 0),     # data gradient of a depth-valid unit: pad 2, 5 -> 7
+    (1, 3, 16, 32, 224, 32, 0, 0),    # the last depth-valid unit (F = 224)
+    (1, 2, 6, 9, 32, 32, 1, 0),       # fewer slices than kd taps
+]
+
+
+def _run(case, dtype, prologue, depth=0, cap=0, seed=0):
+    n, d, h, w, ci, co, pdp, off = case
+    g = torch.Generator().manual_seed(seed)
+    big = torch.randn((n, d, h, w, ci + off + 8), generator=g)
+    x = big[..., off:off + ci]
+    wt = torch.randn((co, ci, 3, 3, 3), generator=g) / (27 * ci) ** 0.5
+    b = torch.randn(co, generator=g)
+    sc = torch.rand(ci, generator=g) + 0.5
+    sh = torch.randn(ci, generator=g) * 0.5
+    pad = (pdp, 1, 1)
+    do = d + 2 * pdp - 2
+    xin = _q(x, dtype)
+    if prologue:
+        xin = torch.relu(xin * sc.double() + sh.double()).to(dtype).double()
+    ref = _ref(xin, _q(wt, dtype), b.double(), pad)
+    ybig = torch.full((n, do, h, w, co + 8), 7.0, dtype=dtype, device=DEV)
+    y = ybig[..., 4:4 + co]
+    kw = dict(prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV)) if prologue else {}
+    F.set_roll_depth(depth)
+    F.set_grid_cap(cap)
+    try:
+        F.conv(big.to(DEV, dtype)[..., off:off + ci], F.pack_weight(wt.to(DEV), 0, dtype), y, (3, 3, 3), pad,
+               bias=b.to(DEV), **kw)
+    finally:
+        F.set_roll_depth(0)
+        F.set_grid_cap(0)
+    torch.cuda.synchronize()
+    # the channels outside the output slice are untouched
+    assert (ybig[..., :4].float() == 7.0).all() and (ybig[..., 4 + co:].float() == 7.0).all()
+    return y.double().cpu(), ref
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("prologue", [False, True])
+@pytest.mark.parametrize("case", CASES)
+def test_roll_forward(case, prologue, dtype):
+    y, ref = _run(case, dtype, prologue)
+    err = (y - ref).abs().max().item()
+    assert err <= _tol(dtype, ref), err
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_roll_tiling_invariant(case):
+    """depth runs of 1, 2, 3 output depths and a capped grid (many tiles per
+    workgroup, the cross-tile DMA walk) give bitwise the default output"""
+    y0, ref = _run(case, torch.bfloat16, True)
+    assert (y0 - ref).abs().max().item() <= _tol(torch.bfloat16, ref)
+    for depth, cap in ((1, 0), (2, 0), (3, 0), (0, 3), (2, 5), (1, 1)):
+        y, _ = _run(case, torch.bfloat16, True, depth, cap)
+        assert torch.equal(y, y0), (depth, cap, (y - y0).abs().max().item())
+
+
+def test_roll_matches_fast_path():
+    """the rolling kernel and the per-kd-stage conv_fast kernel agree within
+    16-bit rounding at a DUF unit shape (and the switch really changes path)"""
+    case = (2, 7, 16, 64, 64, 32, 1, 0)
+    y_roll, ref = _run(case, torch.bfloat16, True)
+    F.set_conv_path("roll", 0)
+    try:
+        y_fast, _ = _run(case, torch.bfloat16, True)
+    finally:
+        F.set_conv_path("roll", -1)
+    tol = _tol(torch.bfloat16, ref)
+    assert (y_roll - ref).abs().max().item() <= tol
+    assert (y_fast - ref).abs().max().item() <= tol
+    assert not torch.equal(y_roll, y_fast)  # different accumulation order: a different kernel ran
+
+
+def test_roll_data_gradient_duf_unit():
+    """dgrad of a depth-valid DUF unit through the public path: dy is a 32-channel
+    slice of the concat gradient, the output the unit's F-channel input gradient"""
+    g = torch.Generator().manual_seed(5)
+    n, d, h, w, f = 1, 7, 16, 32, 96
+    x = torch.randn((n, d, h, w, f), generator=g)
+    wt = torch.randn((32, f, 3, 3, 3), generator=g) / (27 * f) ** 0.5
+    dC = torch.randn((n, d - 2, h, w, 256), generator=g)
+    gy = dC[..., 128:160]
+    xr = _q(x, torch.bfloat16).requires_grad_(True)
+    _ref(xr, _q(wt, torch.bfloat16), None, (0, 1, 1)).backward(_q(gy, torch.bfloat16))
+    dx = torch.empty((n, d, h, w, f), dtype=torch.bfloat16, device=DEV)
+    F.conv(dC.to(DEV, torch.bfloat16)[..., 128:160], F.pack_weight(wt.to(DEV), 1, torch.bfloat16), dx, (3, 3, 3),
+           (2, 1, 1))
+    err = (dx.double().cpu() - xr.grad).abs().max().item()
+    assert err <= _tol(torch.bfloat16, xr.grad), err

@@ -109,6 +109,7 @@ _SIGS = {
     "vsrk_conv_set_algo": (C.c_int, [C.c_int32]),
     "vsrk_conv_set_path": (C.c_int, [C.c_char_p, C.c_int32]),
     "vsrk_conv_set_grid_cap": (C.c_int, [C.c_int32]),
+    "vsrk_conv_set_roll_depth": (C.c_int, [C.c_int32]),
     "vsrk_subpixel_conv_weight": (C.c_int, [_P, _P] + [C.c_int32] * 6 + [_P, _P, _P]),
     "vsrk_subpixel_wgrad_fold": (C.c_int, [_P, _P] + [C.c_int32] * 6 + [_P, _P, C.c_int32, _P]),
     "vsrk_prelu_workspace_size": (C.c_size_t, []),

@@ -1,0 +1,529 @@
+// Rolling-depth implicit-GEMM Conv3d 3x3x3 on MFMA for 16-bit channels-last
+// views (gfx950): the forward of DUF's dense-unit convs nn.Conv3d(F, 32, 3,
+// padding=(p, 1, 1)) (duf_net.py:203,214) and, with a mode-1 packed weight and
+// depth padding 2 - p, their input gradient (loss.backward(),
+// base_trainer.py:128).
+//
+// Why not conv_fast (conv_fast_impl.h), whose stage is (kd tap, 32 input
+// channels): every input slice was staged three times (once per kd tap), the
+// 9-tap weight slice once per stage, and a two-slot ring kept one stage
+// (~1 us of MFMA work) in flight.  PMC on the DUF F->32 conv: MFMA pipes 27 %
+// busy, 35 % of wave time parked at the per-stage vmcnt(0) + barrier, 1.6x the
+// algorithmic HBM bytes.  Here:
+//  * A stage is (input depth slice di, 16 input channels).  The slice is
+//    staged ONCE and feeds all three kd taps: the workgroup keeps three
+//    accumulator banks acc[kd] = output depth di + pd - kd and rotates them
+//    when the walk moves to the next slice (the bank that leaves holds a
+//    finished output depth, which is stored).  Bytes per MFMA: 3.3 B/KFLOP
+//    (was 6.0).
+//  * The stage's weight slab (27 taps x 32 output channels x 16 input
+//    channels) rides in the same slot; taps of a kd with no output depth in
+//    the tile are fetched from the zero page (no L2 traffic).
+//  * Three 48 KB slots: the DMA of stage g+2 is issued while stage g
+//    computes, so two stages (~3 us) of lookahead cover the HBM latency.
+//  * 32-byte LDS rows, the two 16-byte pieces of a row XOR-swizzled by bit 3
+//    of the row's halo column (A) or output channel (B): every ds_read_b128
+//    lane group touches 16 distinct (row mod 8, piece) pairs = all 64 banks.
+//  * Every DMA wave-instruction count is the same for every wave and stage
+//    (47 real 1 KB pieces + 1 junk piece per slot, 6 per wave), so each wait
+//    is a compile-time vmcnt that leaves exactly the next stage in flight.
+//
+// Tile: 8 waves x 2 rows x 32 columns x 32 output channels x a run of output
+// depths [z0, z1) of one sample.  MFMA v_mfma_f32_32x32x16_{bf16,f16},
+// operands "weights x voxels" (a lane's accumulator column is one voxel).
+#include <cstdlib>
+#include "conv_common.h"
+
+namespace {
+using namespace vsrk_conv;
+
+constexpr int RNW = 8;                     // waves (2 per SIMD)
+constexpr int RMS = 2;                     // output rows per wave
+constexpr int RFTH = RNW * RMS;            // 16 tile rows
+constexpr int RHW = TW + 2;                // 34 halo columns
+constexpr int RHROWS = (RFTH + 2) * RHW;   // 612 halo voxels
+constexpr int RCH = 16;                    // input channels per stage
+constexpr int RNAI = (RHROWS + 31) / 32;   // 20 A pieces (32 voxels x 32 B each)
+constexpr int RNBI = 27;                   // 27 B pieces (one tap: 32 channels x 32 B)
+constexpr int RNI = RNAI + RNBI;           // 47
+constexpr int RNQ = (RNI + RNW - 1) / RNW;  // 6 pieces per wave and stage
+constexpr int RSLOT = RNQ * RNW * 1024;    // 48 KB: A | B | one junk piece
+constexpr int RNSLOT = 3;
+
+// Division by a launch constant d (dividends < 2^31): q = (x * mul) >> p with
+// p = 31 + ceil(log2 d), mul = ceil(2^p / d).
+struct RDiv {
+  uint32_t d, mul, p;
+};
+RDiv make_rdiv(int d) {
+  int l = 0;
+  while ((1u << l) < (uint32_t)d) ++l;
+  const uint32_t p = 31 + l;
+  return RDiv{(uint32_t)d, (uint32_t)(((1ull << p) + (uint64_t)d - 1) / (uint64_t)d), p};
+}
+__device__ __forceinline__ int rdiv(int x, const RDiv& f) { return (int)(((uint64_t)(uint32_t)x * f.mul) >> f.p); }
+
+// 32-bit element strides (the host checks that every offset fits)
+struct RView {
+  char* ptr;
+  int d, h, w;
+  int sn, sd, sh, sw;
+};
+
+struct RollArgs {
+  RView x, y;
+  const void* w;
+  const float* bias;
+  const float* pro_scale;
+  const float* pro_shift;
+  int cin, cout, cin_pad, cout_pad;
+  int pd, ph, pw;
+  int prologue;
+  float out_scale;
+  int dzc, nchunk, ntiles;
+  RDiv ntn, nzc, tiles_w, tiles_h;
+};
+
+__device__ __attribute__((aligned(256))) uint4 g_roll_zero[16];
+
+template <int N>
+__device__ __forceinline__ void roll_wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int PRO, int RELU, typename H>
+__global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  float* lbias = reinterpret_cast<float*>(lds + RNSLOT * RSLOT);  // [cout_pad] bias * out_scale
+  float* lsc = lbias + a.cout_pad;                                // [cin_pad] prologue scale / shift
+  float* lsh = lsc + a.cin_pad;
+  if constexpr (PRO) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, a.cin_pad, tid, RNW * 64);
+  for (int i = tid; i < a.cout_pad; i += RNW * 64) lbias[i] = (a.bias && i < a.cout) ? a.bias[i] * a.out_scale : 0.f;
+
+  // ---- per-lane DMA roles, fixed for the launch ----
+  // piece j = wave + RNW*q fills slot bytes [j KB, j+1 KB); lane l writes 16
+  // bytes at j KB + 16 l.  A (j < RNAI): halo voxel v = 32 j + l/2 (row
+  // hh = v / 34, column ww = v % 34), position l & 1 holds the logical piece
+  // p = (l & 1) ^ bit 3 of ww (8 channels).  B (j < RNI): tap j - RNAI,
+  // output channel l/2, piece p = (l & 1) ^ bit 3 of the channel.
+  // qa: the wave's A pieces (bit q); qkd[kd]: its B pieces of taps of depth kd.
+  int rel[RNQ], hwv[RNQ];
+  unsigned qa = 0, qkd0 = 0, qkd1 = 0, qkd2 = 0;
+#pragma unroll
+  for (int q = 0; q < RNQ; ++q) {
+    const int j = wave + RNW * q;
+    rel[q] = 0;
+    hwv[q] = -1;
+    if (j < RNAI) {
+      const int v = 32 * j + (lane >> 1);
+      const int hh = v / RHW, ww = v - (v / RHW) * RHW;
+      const int p = (lane & 1) ^ ((ww >> 3) & 1);
+      rel[q] = hh * a.x.sh + ww * a.x.sw + 8 * p;
+      hwv[q] = v < RHROWS ? ((hh << 8) | ww) : -1;
+      qa |= 1u << q;
+    } else if (j < RNI) {
+      const int co = lane >> 1;
+      const int p = (lane & 1) ^ ((co >> 3) & 1);
+      rel[q] = ((j - RNAI) * a.cout_pad + co) * a.cin_pad + 8 * p;
+      const int kd = (j - RNAI) / 9;
+      if (kd == 0) qkd0 |= 1u << q;
+      else if (kd == 1) qkd1 |= 1u << q;
+      else qkd2 |= 1u << q;
+    }
+  }
+  // ds_read bases (bytes within a slot): A fragment (kw, halo row hr) at
+  // abase[kw] + hr * 34 * 32; B fragment (tap) at RNAI KB + tap KB + bbase.
+  uint32_t abase[3];
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+    abase[kw] = (uint32_t)((wave * RMS * RHW + kw + r) * 32 + 16 * (hf ^ (((kw + r) >> 3) & 1)));
+  const uint32_t bbase = (uint32_t)(RNAI * 1024 + r * 32 + 16 * (hf ^ ((r >> 3) & 1)));
+
+  // ---- tiles of this workgroup (XCD group x owns a contiguous range) ----
+  const int G = gridDim.x;
+  const int xg = blockIdx.x & 7, jb = blockIdx.x >> 3;
+  const int gx = (G >> 3) + (xg < (G & 7) ? 1 : 0);
+  const int cx = xg * (G >> 3) + min(xg, G & 7);
+  const int t_lo = (int)((int64_t)a.ntiles * cx / G);
+  const int t_hi = (int)((int64_t)a.ntiles * (cx + gx) / G);
+
+  // A tile as the walks need it.  Order: output-channel tile fastest (they
+  // share the input), then the depth run, columns, rows, sample.
+  struct RTile {
+    int h0, w0, n0, z0, z1, di_lo, nsl;
+    int xo;  // element offset of halo origin (nb, di = 0, h0 - ph, w0 - pw) in x
+    int yo;  // element offset of (nb, dz = 0, h0, w0, n0) in y
+  };
+  auto decode = [&](int t) __attribute__((always_inline)) {
+    RTile tl;
+    int u = rdiv(t, a.ntn);
+    tl.n0 = (t - u * (int)a.ntn.d) * 32;
+    int v = rdiv(u, a.nzc);
+    tl.z0 = (u - v * (int)a.nzc.d) * a.dzc;
+    u = rdiv(v, a.tiles_w);
+    tl.w0 = (v - u * (int)a.tiles_w.d) * TW;
+    const int nb = rdiv(u, a.tiles_h);
+    tl.h0 = (u - nb * (int)a.tiles_h.d) * RFTH;
+    tl.z1 = min(tl.z0 + a.dzc, a.y.d);
+    tl.di_lo = max(0, tl.z0 - a.pd);
+    tl.nsl = min(a.x.d - 1, tl.z1 + 1 - a.pd) - tl.di_lo + 1;
+    tl.xo = nb * a.x.sn + (tl.h0 - a.ph) * a.x.sh + (tl.w0 - a.pw) * a.x.sw;
+    tl.yo = nb * a.y.sn + tl.h0 * a.y.sh + tl.w0 * a.y.sw + tl.n0;
+    return tl;
+  };
+  // spatial validity of this lane's A pieces for a tile (bit q)
+  auto tile_mask = [&](const RTile& tl) __attribute__((always_inline)) {
+    const int hb = tl.h0 - a.ph, wb = tl.w0 - a.pw;
+    unsigned m = 0;
+#pragma unroll
+    for (int q = 0; q < RNQ; ++q) {
+      const int hh = hwv[q] >> 8, ww = hwv[q] & 0xff;
+      const bool ok = hwv[q] >= 0 && (unsigned)(hb + hh) < (unsigned)a.x.h && (unsigned)(wb + ww) < (unsigned)a.x.w;
+      m |= (ok ? 1u : 0u) << q;
+    }
+    return m;
+  };
+  // kd taps with an output depth inside [z0, z1) for input slice di
+  auto kd_mask = [&](int z0, int z1, int di) __attribute__((always_inline)) {
+    const int P = di + a.pd;
+    return (P >= z0 && P < z1 ? 1u : 0u) | (P - 1 >= z0 && P - 1 < z1 ? 2u : 0u) |
+           (P - 2 >= z0 && P - 2 < z1 ? 4u : 0u);
+  };
+
+  // ---- the DMA walk (two stages ahead of the compute walk) ----
+  struct Walk {
+    int t, sl, c;
+    RTile tl;
+    unsigned m;  // lane mask (VGPR)
+  };
+  auto advance = [&](Walk& k) __attribute__((always_inline)) -> bool {
+    if (++k.c < a.nchunk) return true;
+    k.c = 0;
+    if (++k.sl < k.tl.nsl) return true;
+    k.sl = 0;
+    k.t += gx;
+    if (k.t >= t_hi) return false;
+    k.tl = decode(k.t);
+    k.m = tile_mask(k.tl);
+    return true;
+  };
+  const char* zp = reinterpret_cast<const char*>(g_roll_zero);
+  struct Dma {
+    const H* xb;
+    const H* wsrc;
+    unsigned use;  // bit q: the piece reads its source (else the zero page)
+  };
+  // stage of walk k: A pieces of slice di, channels [c0, c0 + 16) (zero page
+  // outside the image), B pieces of the weight slab (zero page for taps of a
+  // kd with no output depth in the tile), and the junk piece (zero page)
+  auto prep = [&](const Walk& k) __attribute__((always_inline)) {
+    Dma d;
+    const int di = k.tl.di_lo + k.sl;
+    const int c0 = k.c * RCH;
+    d.xb = reinterpret_cast<const H*>(a.x.ptr) + (k.tl.xo + di * a.x.sd + c0);
+    d.wsrc = reinterpret_cast<const H*>(a.w) + (k.tl.n0 * a.cin_pad + c0);
+    const unsigned km = kd_mask(k.tl.z0, k.tl.z1, di);
+    d.use = (k.m & qa) | ((km & 1) ? qkd0 : 0u) | ((km & 2) ? qkd1 : 0u) | ((km & 4) ? qkd2 : 0u);
+    return d;
+  };
+  auto dma = [&](const Dma& d, int q, int slot) __attribute__((always_inline)) {
+    const int j = wave + RNW * q;
+    const H* base = ((qa >> q) & 1) ? d.xb : d.wsrc;
+    const void* src = ((d.use >> q) & 1) ? (const void*)(base + rel[q]) : (const void*)zp;
+    glds16(src, lds_addr(lds) + slot * RSLOT + j * 1024);
+  };
+
+  f32x16 acc[3][RMS];  // bank b: the output depth dz with dz % 3 == b
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int m = 0; m < RMS; ++m)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[k][m][i] = 0.f;
+
+  // One stage on slot SLOT: the A fragments of all three kw (4 halo rows
+  // each) are read once; then per bank b (kd = the tap whose output depth
+  // lives in bank b) and kw, 3 B fragments and 6 MFMAs, B software-pipelined
+  // one group ahead (read unconditionally: an idle kd's taps are zeros).  The
+  // DMA pieces of the stage two ahead are issued in the first groups.
+  auto compute = [&](auto slot_c, int P, unsigned km, const Dma& dn, bool don) __attribute__((always_inline)) {
+    constexpr int SLOT = decltype(slot_c)::value;
+    const char* sl = lds + SLOT * RSLOT;
+    uint4 ax[3][RMS + 2];
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+      for (int hr = 0; hr < RMS + 2; ++hr)
+        ax[kw][hr] = *reinterpret_cast<const uint4*>(sl + abase[kw] + hr * RHW * 32);
+    const int pm = P % 3;
+    uint32_t bofs[3];  // byte offset of the taps of the kd whose output depth is in bank b
+#pragma unroll
+    for (int b = 0; b < 3; ++b) bofs[b] = (uint32_t)(((pm + 3 - b) % 3) * 9 * 1024);
+    const unsigned bm = ((km & 1) ? (1u << pm) : 0u) | ((km & 2) ? (1u << ((pm + 2) % 3)) : 0u) |
+                        ((km & 4) ? (1u << ((pm + 1) % 3)) : 0u);  // banks with work
+    uint4 bw[2][3];
+    auto load_b = [&](uint4* bf, int g) __attribute__((always_inline)) {
+      const int b = g / 3, kw = g % 3;
+      const char* pb = sl + bbase + bofs[b] + kw * 1024;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) bf[kh] = *reinterpret_cast<const uint4*>(pb + kh * 3 * 1024);
+    };
+    load_b(bw[0], 0);
+#pragma unroll
+    for (int g = 0; g < 9; ++g) {
+      if (g + 1 < 9) load_b(bw[(g + 1) & 1], g + 1);
+      if (g < RNQ && don) dma(dn, g, (SLOT + 2) % 3);
+      const int b = g / 3, kw = g % 3;
+      if ((bm >> b) & 1) {
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+          for (int ms = 0; ms < RMS; ++ms) mma<H>(acc[b][ms], bw[g & 1][kh], ax[kw][ms + kh]);
+      }
+    }
+  };
+
+  // Epilogue of one finished output depth dz of a tile: out = [relu](acc *
+  // out_scale + bias * out_scale), 4 channels (8 bytes) per lane.
+  const float osc = a.out_scale;
+  auto epilogue = [&](const f32x16 (&A)[RMS], const RTile& tl, int dz) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ms = 0; ms < RMS; ++ms) {
+      const int ho = tl.h0 + wave * RMS + ms, wo = tl.w0 + r;
+      if (ho < a.y.h && wo < a.y.w) {
+        H* yp = reinterpret_cast<H*>(a.y.ptr) + (tl.yo + dz * a.y.sd + (wave * RMS + ms) * a.y.sh + r * a.y.sw + 4 * hf);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int co = tl.n0 + 8 * g + 4 * hf;
+          if (co < a.cout) {
+            const float4 bs = *reinterpret_cast<const float4*>(lbias + co);
+            float v[4] = {fmaf(A[ms][4 * g + 0], osc, bs.x), fmaf(A[ms][4 * g + 1], osc, bs.y),
+                          fmaf(A[ms][4 * g + 2], osc, bs.z), fmaf(A[ms][4 * g + 3], osc, bs.w)};
+            if constexpr (RELU) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+            }
+            *reinterpret_cast<uint2*>(yp + 8 * g) = pack_pk<H, uint2>(v);
+          }
+        }
+      }
+    }
+  };
+  // Flush after slice pdi of tile tl: the banks whose output depth takes no
+  // more contributions -- dz = pdi + pd - 2 when the walk stays in the tile
+  // (all = false), every bank at the end of the tile -- are stored (if inside
+  // the tile's depth run) and zeroed.
+  auto flush = [&](const RTile& tl, int pdi, bool all) __attribute__((always_inline)) {
+    const int P = pdi + a.pd;
+    const int bdone = (P + 1) % 3;  // bank of P - 2
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      if (all || b == bdone) {
+        const int dz = P - (P + 3 - b) % 3;  // the output depth in bank b
+        if (dz >= tl.z0 && dz < tl.z1) epilogue(acc[b], tl, dz);
+#pragma unroll
+        for (int m = 0; m < RMS; ++m)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) acc[b][m][i] = 0.f;
+      }
+    }
+  };
+  // BN-affine/ReLU prologue on this lane's own landed A pieces (in-image ones;
+  // the halo stays zero as in the reference, which pads relu(bn(x)))
+  const bool relu_in = (a.prologue & VSRK_PRO_RELU) != 0;
+  auto transform = [&](auto slot_c, int c, unsigned m) __attribute__((always_inline)) {
+    constexpr int SLOT = decltype(slot_c)::value;
+    const int c0 = c * RCH;
+#pragma unroll
+    for (int q = 0; q < RNQ; ++q) {
+      const int j = wave + RNW * q;
+      if (((qa & m) >> q) & 1) {
+        uint4* p = reinterpret_cast<uint4*>(lds + SLOT * RSLOT + j * 1024 + lane * 16);
+        const int ww = hwv[q] & 0xff;
+        *p = prologue_lds<H>(*p, c0 + 8 * ((lane & 1) ^ ((ww >> 3) & 1)), relu_in, lsc, lsh);
+      }
+    }
+  };
+
+  // compute walk: tile ct (decoded when the walk enters it), slice cs, chunk cc
+  int t = t_lo + jb;
+  if (t >= t_hi) return;
+  Walk nx;
+  nx.t = t;
+  nx.sl = 0;
+  nx.c = 0;
+  nx.tl = decode(t);
+  nx.m = tile_mask(nx.tl);
+  RTile ct = nx.tl;
+  unsigned cm = nx.m;
+  int cs = 0, cc = 0;
+  {
+    const Dma d0 = prep(nx);
+#pragma unroll
+    for (int q = 0; q < RNQ; ++q) dma(d0, q, 0);
+  }
+  bool vn = advance(nx);
+  if (vn) {
+    const Dma d1 = prep(nx);
+#pragma unroll
+    for (int q = 0; q < RNQ; ++q) dma(d1, q, 1);
+    vn = advance(nx);
+  }
+  __syncthreads();  // bias / prologue tables visible
+  RTile ptl = ct;
+  int pdi = -1;     // slice whose end is still to be flushed (-1: none)
+  bool pall = false;
+  // one stage; false when it was the workgroup's last
+  auto step = [&](auto slot_c) __attribute__((always_inline)) -> bool {
+    const bool more = cc + 1 < a.nchunk || cs + 1 < ct.nsl || t + gx < t_hi;
+    if (more) roll_wait_vmcnt<RNQ>();  // this stage landed; the next stays in flight
+    else roll_wait_vmcnt<0>();
+    if constexpr (PRO) transform(slot_c, cc, cm);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // this slot ready, the previous one free
+    if (pdi >= 0) flush(ptl, pdi, pall);
+    const int di = ct.di_lo + cs;
+    Dma dn;
+    dn.xb = nullptr;
+    dn.wsrc = nullptr;
+    dn.use = 0;
+    if (vn) dn = prep(nx);
+    compute(slot_c, di + a.pd, kd_mask(ct.z0, ct.z1, di), dn, vn);
+    if (vn) vn = advance(nx);
+    // advance the compute walk; a finished slice is flushed after the next barrier
+    pdi = -1;
+    if (++cc < a.nchunk) return true;
+    cc = 0;
+    ptl = ct;
+    pdi = di;
+    pall = false;
+    if (++cs < ct.nsl) return true;
+    cs = 0;
+    pall = true;
+    t += gx;
+    if (t >= t_hi) return false;
+    ct = decode(t);
+    cm = tile_mask(ct);
+    return true;
+  };
+  while (step(std::integral_constant<int, 0>{}) && step(std::integral_constant<int, 1>{}) &&
+         step(std::integral_constant<int, 2>{})) {
+  }
+  flush(ptl, pdi, true);
+}
+
+int g_roll_mode = -1;  // -1: from VSRK_CONV_ROLL (default on), 0 off, 1 on
+int g_roll_dz = 0;     // > 0: output depths per tile (test knob), 0: automatic
+
+int roll_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+template <int PRO, int RELU, typename H>
+int launch_roll(const RollArgs& a, size_t lds, int grid, hipStream_t s) {
+  auto kern = conv_roll_kernel<PRO, RELU, H>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  kern<<<grid, RNW * 64, lds, s>>>(a);
+  VSRK_LAUNCH_CHECK("conv_fwd(roll)");
+  return VSRK_OK;
+}
+
+}  // namespace
+
+extern "C" int vsrk_conv_set_roll_depth(int32_t depths) {
+  VSRK_CHECK(depths >= 0, "conv_set_roll_depth: depths must be >= 0");
+  g_roll_dz = depths;
+  return VSRK_OK;
+}
+
+void vsrk_conv_set_roll_mode(int mode) { g_roll_mode = mode; }
+
+// 1 = launched, 0 = not eligible, < 0 = -(error status)
+int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                       const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
+                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s) {
+  if (g_roll_mode < 0) {
+    const char* e = getenv("VSRK_CONV_ROLL");
+    g_roll_mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (g_roll_mode == 0) return 0;
+  if (!vsrk_is16(x->dtype) || y->dtype != x->dtype) return 0;
+  if (d->kd != 3 || d->kh != 3 || d->kw != 3) return 0;
+  if (residual || mask || d->accumulate || d->bias_perm_r > 1 || d->act == VSRK_ACT_PRELU) return 0;
+  if (x->shuffle > 1 || y->shuffle > 1) return 0;
+  if (x->c % RCH != 0 || !chunk_ok(x, 2)) return 0;
+  if (d->pd < 0 || d->pd > 2 || d->ph < 0 || d->ph > 2 || d->pw < 0 || d->pw > 2) return 0;
+  if (y->d != x->d + 2 * d->pd - 2 || y->h != x->h + 2 * d->ph - 2 || y->w != x->w + 2 * d->pw - 2) return 0;
+  if (y->c % 4 != 0 || ((uintptr_t)y->ptr) % 8 != 0 || y->sn % 4 || y->sd % 4 || y->sh % 4 || y->sw % 4) return 0;
+  for (const vsrk_tensor5* t : {x, y}) {  // every element offset fits in 32 bits
+    const int64_t span = (int64_t)(t->n - 1) * t->sn + (int64_t)(t->d - 1) * t->sd + (int64_t)(t->h - 1) * t->sh +
+                         (int64_t)(t->w - 1) * t->sw + t->c + 2 * (int64_t)RHW * t->sw + (RFTH + 2) * t->sh;
+    if (span >= (1ll << 31) || t->sn < 0 || t->sd < 0 || t->sh < 0 || t->sw < 0) return 0;
+  }
+  auto rview = [](const vsrk_tensor5* t) {
+    RView v;
+    v.ptr = (char*)t->ptr;
+    v.d = t->d; v.h = t->h; v.w = t->w;
+    v.sn = (int)t->sn; v.sd = (int)t->sd; v.sh = (int)t->sh; v.sw = (int)t->sw;
+    return v;
+  };
+  RollArgs a;
+  a.x = rview(x);
+  a.y = rview(y);
+  a.w = w_packed;
+  a.bias = bias;
+  a.pro_scale = pro_scale;
+  a.pro_shift = pro_shift;
+  a.cin = x->c;
+  a.cout = y->c;
+  a.cin_pad = round_up(x->c, 32);
+  a.cout_pad = round_up(y->c, 128);
+  a.pd = d->pd;
+  a.ph = d->ph;
+  a.pw = d->pw;
+  a.prologue = d->prologue;
+  a.out_scale = d->out_scale;
+  a.nchunk = x->c / RCH;
+  const int tiles_h = ceil_div(y->h, RFTH), tiles_w = ceil_div(y->w, TW), ntn = ceil_div(y->c, 32);
+  const int64_t spatial = (int64_t)y->n * tiles_h * tiles_w * ntn;
+  if (spatial == 0 || y->d == 0) return 1;
+  // Depth run per tile: as long as possible (each input slice then serves
+  // three output depths) while the grid still gets >= 2 tiles per CU.
+  int dzc = y->d;
+  if (g_roll_dz > 0) {
+    dzc = std::min(g_roll_dz, y->d);
+  } else {
+    const int64_t want = 2 * (int64_t)roll_num_cus();
+    if (spatial < want) {
+      const int64_t runs = std::min<int64_t>(ceil_div64(want, spatial), y->d);
+      dzc = (int)ceil_div64(y->d, runs);
+    }
+  }
+  a.dzc = dzc;
+  const int nzc = ceil_div(y->d, dzc);
+  a.ntn = make_rdiv(ntn);
+  a.nzc = make_rdiv(nzc);
+  a.tiles_w = make_rdiv(tiles_w);
+  a.tiles_h = make_rdiv(tiles_h);
+  const int64_t ntiles = spatial * nzc;
+  VSRK_CHECK(ntiles < (1ll << 31), "conv_fwd(roll): too many tiles");
+  a.ntiles = (int)ntiles;
+  const size_t lds = (size_t)RNSLOT * RSLOT + (size_t)a.cout_pad * 4 + (d->prologue ? 2 * (size_t)a.cin_pad * 4 : 0);
+  if (lds > 160 * 1024) return 0;
+  const int grid = (int)vsrk_capped_grid(std::min<int64_t>(ntiles, roll_num_cus()));
+  const bool relu = d->act == VSRK_ACT_RELU;
+  int rc = vsrk_dispatch16(x->dtype, [&](auto tag) {
+    using H = decltype(tag);
+    if (d->prologue) return relu ? launch_roll<1, 1, H>(a, lds, grid, s) : launch_roll<1, 0, H>(a, lds, grid, s);
+    return relu ? launch_roll<0, 1, H>(a, lds, grid, s) : launch_roll<0, 0, H>(a, lds, grid, s);
+  });
+  return rc == VSRK_OK ? 1 : -rc;
+}

@@ -26,6 +26,13 @@ int vsrk_conv_fwd_k3(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
                      const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                      const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
 
+// rolling-depth 16-bit Conv3d 3x3x3 (conv_roll.hip): forward / data gradient;
+// same return convention; vsrk_conv_set_roll_mode: -1 env VSRK_CONV_ROLL, 0 off, 1 on
+int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                       const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
+                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
+void vsrk_conv_set_roll_mode(int mode);
+
 // pointwise (1x1x1) bf16 conv (conv_pw.hip): forward / data gradient and
 // weight gradient; same return convention (the wgrad launches its own reduce)
 int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,

@@ -210,6 +210,12 @@ def set_conv_path(path: str, mode: int) -> None:
     N.check(_lib().vsrk_conv_set_path(path.encode(), int(mode)), "conv_set_path")
 
 
+def set_roll_depth(depths: int) -> None:
+    """Test knob: output depths per tile of the rolling-depth Conv3d 3x3x3
+    kernel (0 = automatic)."""
+    N.check(_lib().vsrk_conv_set_roll_depth(int(depths)), "conv_set_roll_depth")
+
+
 def set_grid_cap(max_workgroups: int) -> None:
     """Cap the persistent conv grids / wgrad split (0 = default); tests use it to
     run many tiles per workgroup at small shapes."""
