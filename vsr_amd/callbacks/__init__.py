@@ -1,5 +1,10 @@
 """Callbacks with the reference's interface (src/callbacks): the checkpoint
-Monitor.  The TensorBoard loggers stay the reference's (rank 0 only)."""
+Monitor and the per-epoch loggers (TensorBoard when importable, else plain
+files; rank 0 only)."""
+from . import loggers
+from .loggers import (AcdcMISRLogger, AcdcSISRLogger, AcdcSISRSRFBLogger, AcdcVSRLogger, BaseLogger, Dsb15MISRLogger,
+                      Dsb15SISRLogger, Dsb15SISRSRFBLogger, Dsb15VSRLogger)
 from .monitor import Monitor
 
-__all__ = ["Monitor"]
+__all__ = ["Monitor", "loggers", "BaseLogger", "AcdcSISRLogger", "AcdcSISRSRFBLogger", "AcdcMISRLogger",
+           "AcdcVSRLogger", "Dsb15SISRLogger", "Dsb15SISRSRFBLogger", "Dsb15MISRLogger", "Dsb15VSRLogger"]
