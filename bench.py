@@ -242,7 +242,8 @@ def run_model(name, args, world, rank, dev):
         loss.backward()
         if sync is not None:
             sync.finish()
-        opt.step()
+        if graph or net.step_ok():  # fp16: skip a step whose gradients overflowed (eager only)
+            opt.step()
         return loss
 
     match, kdesc = dominant(name, args.precision)

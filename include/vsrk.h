@@ -111,14 +111,13 @@ int vsrk_conv_fwd(const vsrk_conv_desc* desc, const vsrk_tensor5* x, const void*
 int vsrk_conv_set_algo(int32_t mode);
 
 /* Per-path switch for A/B measurement and tests: path "fast" (bf16 LDS-DMA
- * conv, default on), "k3" (its second-generation 3x3(x3) kernel: two
- * workgroups per CU, buffer-load DMA; opt-in, within "fast"), "pw"
+ * conv, default on), "pw"
  * (bf16 1x1x1 convs with cin = cout or cout a multiple of cin, cin <= 256:
  * forward, data gradient and weight gradient in one pass over HBM, default
  * on), "thin" (cin <= 4 / cout <= 3 kernels incl. their weight gradient,
- * default on), "wgrad_fast" (LDS-DMA weight gradient, default off); mode -1 =
- * default/environment (VSRK_CONV_FAST, VSRK_CONV_K3, VSRK_CONV_PW,
- * VSRK_CONV_THIN, VSRK_WGRAD_FAST), 0 = off, 1 = on where eligible.  Every path computes the
+ * default on), "wgrad_pipe" (pipelined 16-bit 3x3(x3) weight gradient, default
+ * on); mode -1 = default/environment (VSRK_CONV_FAST, VSRK_CONV_PW,
+ * VSRK_CONV_ROLL, VSRK_CONV_THIN, VSRK_WGRAD_PIPE), 0 = off, 1 = on where eligible.  Every path computes the
  * same result as the generic kernels within bf16 rounding. */
 int vsrk_conv_set_path(const char* path, int32_t mode);
 

@@ -13,40 +13,16 @@ tests/test_configs_gpu.py runs an epoch.
 """
 from pathlib import Path
 
-import numpy as np
 import pytest
 import torch
 import yaml
 
+from nifti_tree import make_tree
 from vsr_amd import config as C
-from vsr_amd.data import nifti
 
 ROOT = Path(__file__).resolve().parent.parent
 REF = Path("/root/reference/configs")
 OWN = sorted((ROOT / "configs" / "train").glob("*.yaml"))
-
-
-def make_tree(root: Path, T=30, H=32, W=32, patients=2, seed=0):
-    """acdc_preprocess.py:55-85 layout: imgs/{split}/{HR,LR/X{r}}/<patient>/*_2d_slice*_frame*.nii.gz
-    and videos/{split}/.../*_2d+1d_sequence*.nii.gz, r = 2 and 4, T = 30 (DSB15 keeps
-    sequences of >= 30 frames, dsb15_preprocess.py:28)."""
-    rng = np.random.default_rng(seed)
-    for split in ("train", "valid", "test"):
-        for i in range(patients):
-            pid = f"patient{i:03d}"
-            hr = rng.integers(0, 255, (H, W, 1, T)).astype(np.float32)
-            vols = [(hr, "HR")]
-            for r in (2, 4):
-                vols.append((hr.reshape(H // r, r, W // r, r, 1, T).mean(axis=(1, 3)).astype(np.float32), f"LR/X{r}"))
-            for vol, sub in vols:
-                d = root / "videos" / split / sub / pid
-                d.mkdir(parents=True, exist_ok=True)
-                nifti.save(vol, d / f"{pid}_2d+1d_sequence00.nii.gz")
-                d = root / "imgs" / split / sub / pid
-                d.mkdir(parents=True, exist_ok=True)
-                for t in range(T):
-                    nifti.save(vol[..., t], d / f"{pid}_2d_slice00_frame{t:02d}.nii.gz")
-    return root
 
 
 def _point_data(cfg, tree: Path):

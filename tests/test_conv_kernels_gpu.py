@@ -332,64 +332,6 @@ def test_thin_wgrad(case, prologue):
     assert eb <= 1e-2 * (1 + br.grad.abs().max().item()), eb
 
 
-@pytest.mark.parametrize("r", [2, 3])
-def test_wgrad_fast_shuffle_prologue(r):
-    """LDS-DMA wgrad path with a sub-pixel dy view of 32-channel planes and a prologue."""
-    g = torch.Generator().manual_seed(24)
-    bf = torch.bfloat16
-    n, h, w, ci, f = 2, 9, 21, 64, 32
-    co = f * r * r
-    x = torch.randn((n, 1, h, w, ci), generator=g)
-    sc = torch.rand(ci, generator=g) + 0.5
-    sh = torch.randn(ci, generator=g)
-    wt = torch.randn((co, ci, 3, 3), generator=g) / 24
-    gy = torch.randn((n, f, h * r, w * r), generator=g)
-    xin = torch.relu(_q(x, bf) * sc.double() + sh.double()).to(bf).double()
-    wr = _q(wt, bf).requires_grad_(True)
-    br = torch.zeros(co, dtype=torch.float64, requires_grad=True)
-    y = Fn.pixel_shuffle(Fn.conv2d(xin[:, 0].permute(0, 3, 1, 2), wr, br, padding=1), r)
-    y.backward(_q(gy, bf))
-    dw = torch.empty((co, ci, 3, 3), device=DEV)
-    db = torch.empty(co, device=DEV)
-    gy_cl = gy.permute(0, 2, 3, 1).unsqueeze(1).contiguous().to(DEV, bf)
-    F.set_conv_path("wgrad_fast", 1)
-    try:
-        F.conv_wgrad(x.to(DEV, bf), gy_cl, (1, 3, 3), (0, 1, 1), dw.view(co, ci, 1, 3, 3), db,
-                     prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV), perm_r=r, dy_shuffle=r)
-    finally:
-        F.set_conv_path("wgrad_fast", -1)
-    err = (dw.double().cpu() - wr.grad).abs().max().item()
-    eb = (db.double().cpu() - br.grad).abs().max().item()
-    assert err <= 1e-2 * (1 + wr.grad.abs().max().item()), err
-    assert eb <= 1e-2 * (1 + br.grad.abs().max().item()), eb
-
-
-@pytest.mark.parametrize("case", [c for c in CASES if c[4] % 8 == 0 and c[5] % 8 == 0])
-def test_wgrad_fast_path(case):
-    """the LDS-DMA weight-gradient kernel (opt-in path) against fp64 autograd."""
-    n, d, h, w, ci, co, k, pad = case
-    bf = torch.bfloat16
-    g = torch.Generator().manual_seed(25)
-    x = torch.randn((n, d, h, w, ci), generator=g)
-    wt = torch.randn((co, ci, *k), generator=g) / (ci * k[0] * k[1] * k[2]) ** 0.5
-    do = d + 2 * pad[0] - k[0] + 1
-    gy = torch.randn((n, do, h, w, co), generator=g)
-    wr = _q(wt, bf).requires_grad_(True)
-    br = torch.zeros(co, dtype=torch.float64, requires_grad=True)
-    _ref_conv(_q(x, bf), wr, br, pad).backward(_q(gy, bf))
-    dw = torch.empty((co, ci, *k), device=DEV)
-    db = torch.empty(co, device=DEV)
-    F.set_conv_path("wgrad_fast", 1)
-    try:
-        F.conv_wgrad(x.to(DEV, bf), gy.to(DEV, bf), k, pad, dw, db)
-    finally:
-        F.set_conv_path("wgrad_fast", -1)
-    ew = (dw.double().cpu() - wr.grad).abs().max().item()
-    eb = (db.double().cpu() - br.grad).abs().max().item()
-    assert ew <= 1e-2 * (1 + wr.grad.abs().max().item()), ew
-    assert eb <= 1e-2 * (1 + br.grad.abs().max().item()), eb
-
-
 @pytest.mark.parametrize("case", THIN_FWD)
 def test_thin_matches_generic(case):
     """thin-channel kernels == the generic implicit-GEMM kernels on the same bf16 operands

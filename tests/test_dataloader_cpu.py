@@ -71,3 +71,13 @@ def test_bench_rejects_gpus_world_mismatch():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "1", "--steps", "1"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 2 and "disagrees" in r.stderr
+
+
+def test_shard_sampler_unpadded():
+    """validation / test shards: contiguous, disjoint, no repeated samples."""
+    from vsr_amd.data.dataloader import ShardSampler
+    ds = list(range(10))
+    parts = [list(ShardSampler(ds, num_replicas=3, rank=r)) for r in range(3)]
+    assert sum(parts, []) == ds
+    assert [len(p) for p in parts] == [3, 3, 4]
+    assert all(len(ShardSampler(ds, 3, r)) == len(parts[r]) for r in range(3))

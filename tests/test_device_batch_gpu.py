@@ -1,7 +1,9 @@
 """GPU batch gather (include/vsrk_data.h, vsr_amd.data.DeviceCineBatcher)
 against the CPU pipeline it replaces: the reference's windowing
 (acdc_{misr,vsr}_dataset.py) and numpy augments (transforms.py:321-450)
-under the same Python `random` seed.  Pure gathers: bit-exact."""
+under the same Python `random` seed -- the build's CPU restatement, and the
+reference's own code through the committed fixture tests/golden/data_path.pt
+(oracle/make_data_golden.py).  Pure gathers: bit-exact."""
 import random
 
 import numpy as np
@@ -68,3 +70,40 @@ def test_gather_without_augments_and_normalize():
     assert torch.allclose(got, ref, rtol=0, atol=1e-5)
     with pytest.raises(ValueError):
         DeviceCineBatcher(lr.cuda(), hr.cuda(), "vsr", augments=[T.Normalize([0.0], [1.0])])
+
+
+def _golden():
+    from pathlib import Path
+    return torch.load(Path(__file__).resolve().parent / "golden" / "data_path.pt", weights_only=True)
+
+
+@pytest.mark.parametrize("name", ["misr_middle5_train", "misr_last4_train", "vsr_last3_train", "vsr_middle5_train",
+                                  "sisr_train"])
+def test_gather_matches_reference_fixture(name):
+    """vsrk_gather_windows against the reference's own Dataset + transforms
+    (tests/golden/data_path.pt, oracle/make_data_golden.py): bitwise, per
+    sample under the fixture's Python `random` seed."""
+    import re
+    fx = _golden()
+    case = next(c for c in fx["cases"] if c["name"] == name)
+    lr = torch.stack([v["lr"][:, :, 0].permute(2, 0, 1) for v in fx["volumes"]]).cuda()  # (V, T, h, w)
+    hr = torch.stack([v["hr"][:, :, 0].permute(2, 0, 1) for v in fx["volumes"]]).cuda()
+    task = {"AcdcMISRDataset": "misr", "AcdcVSRDataset": "vsr", "AcdcSISRDataset": "sisr"}[case["cls"]]
+    kw = case["kwargs"]
+    b = DeviceCineBatcher(lr, hr, task, num_frames=kw.get("num_frames", 1), temporal_order=kw.get("temporal_order"),
+                          augments=fx["augments"], normalize=(54.089, 48.084))
+    for seed, entry, want in zip(case["seeds"], case["data"], case["samples"]):
+        vol = int(re.search(r"patient(\d+)", entry[0]).group(1)) - 1
+        t = int(entry[1]) if len(entry) > 1 else int(re.search(r"frame(\d+)", entry[0]).group(1)) - 1
+        random.seed(seed)
+        out = b([(vol, t)])
+        if task == "sisr":
+            assert torch.equal(out["lr_img"][0].cpu(), want["lr_img"])
+            assert torch.equal(out["hr_img"][0].cpu(), want["hr_img"])
+            continue
+        got = torch.stack([x[0] for x in out["lr_imgs"]]).cpu()
+        assert torch.equal(got, want["lr_imgs"]), (name, seed)
+        if task == "misr":
+            assert torch.equal(out["hr_img"][0].cpu(), want["hr_img"])
+        else:
+            assert torch.equal(torch.stack([x[0] for x in out["hr_imgs"]]).cpu(), want["hr_imgs"])

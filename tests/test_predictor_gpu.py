@@ -81,3 +81,60 @@ def test_predictor_rejects_batched_loader():
     loader = DataLoader(SyntheticCine("sisr", volumes=1, frames=2, size=(8, 8), upscale_factor=2), batch_size=2)
     with pytest.raises(ValueError):
         predictors.AcdcSISRPredictor(DEV, loader, net, [losses.L1Loss()], [1.0], [metrics.PSNR()])
+
+
+@pytest.mark.parametrize("kind", ["sisr", "misr"])
+def test_export_names_follow_the_reference(kind, tmp_path):
+    """ACDC file names (acdc_preprocess.py:70-85) through the SISR / MISR
+    predictors: rows named as acdc_{sisr,misr}_predictor.py:66-68 /
+    acdc_misr_predictor.py:67-69, one PNG per frame
+    imgs/<patient>/<slice>_<frame>.png (no overwrites), one GIF per sequence
+    videos/<patient>/<sequence>.gif; a reference checkpoint (pickled Monitor)
+    loads through the allow-list."""
+    import sys
+    import types
+    from nifti_tree import make_tree
+    from vsr_amd.callbacks.monitor import Monitor
+    from vsr_amd.data import AcdcMISRDataset, AcdcSISRDataset
+
+    T = 4
+    root = make_tree(tmp_path / "data", T=T, H=16, W=16, patients=2)
+    tf = [{"name": "Normalize", "kwargs": {"means": [54.089], "stds": [48.084]}}, {"name": "ToTensor"}]
+    if kind == "sisr":
+        ds = AcdcSISRDataset(downscale_factor=2, transforms=tf, data_dir=root / "imgs", type="test")
+        net = nets.EDSRNet(1, 1, num_resblocks=1, num_features=16, upscale_factor=2)
+        cls = predictors.AcdcSISRPredictor
+    else:
+        ds = AcdcMISRDataset(downscale_factor=2, transforms=tf, num_frames=7, data_dir=root / "videos", type="test")
+        net = nets.DUFNet(1, 1, num_frames=7, size_filter=5, upscale_factor=2, backbone="_DenseLayer16")
+        cls = predictors.AcdcMISRPredictor
+    net = net.to(DEV).set_precision("fp32")
+    # a checkpoint in the reference's format: the Monitor pickled under src.callbacks.monitor
+    mod = types.ModuleType("src.callbacks.monitor")
+    mod.Monitor = type("Monitor", (), {})
+    for name in ("src", "src.callbacks"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["src.callbacks.monitor"] = mod
+    try:
+        ref_mon = mod.Monitor()
+        ref_mon.__dict__.update(checkpoints_dir=tmp_path / "ck", mode="min", target="Loss", saved_freq=1,
+                                early_stop=0, best=1.0, not_improved_count=0)
+        torch.save({"net": net.state_dict(), "monitor": ref_mon, "epoch": 1}, tmp_path / "model_best.pth")
+    finally:
+        for name in ("src.callbacks.monitor", "src.callbacks", "src"):
+            sys.modules.pop(name, None)
+    loader = DataLoader(ds, batch_size=1, shuffle=False)
+    out = tmp_path / "pred"
+    pred = cls(DEV, loader, net, [losses.L1Loss()], [1.0], [metrics.PSNR()], saved_dir=out, exported=True)
+    pred.load(tmp_path / "model_best.pth")
+    pred.predict()
+    rows = list(csv.reader(open(out / "results.csv")))
+    names = [r[0] for r in rows[1:]]
+    want = [f"patient{p:03d}_2d_slice01_frame{t + 1:02d}" for p in range(2) for t in range(T)]
+    assert names == want
+    pngs = sorted(str(p.relative_to(out / "imgs")) for p in (out / "imgs").rglob("*.png"))
+    assert pngs == sorted(f"patient{p:03d}/slice01_frame{t + 1:02d}.png" for p in range(2) for t in range(T))
+    gifs = sorted(str(p.relative_to(out / "videos")) for p in (out / "videos").rglob("*.gif"))
+    assert gifs == [f"patient{p:03d}/sequence01.gif" for p in range(2)]
+    from PIL import Image
+    assert Image.open(out / "videos" / "patient000" / "sequence01.gif").n_frames == T

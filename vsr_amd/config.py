@@ -193,7 +193,7 @@ def build_train(config, device=None):
     train_bs, valid_bs = dl.kwargs.pop('train_batch_size'), dl.kwargs.pop('valid_batch_size')
     dl.kwargs.update(collate_fn=_collate(config.dataset), batch_size=train_bs)
     train_loader = get_instance(ns['data'], dl, train_dataset)
-    dl.kwargs.update(batch_size=valid_bs)
+    dl.kwargs.update(batch_size=valid_bs, shard_padding=False)  # no repeated samples in the metrics
     valid_loader = get_instance(ns['data'], dl, valid_dataset)
     net = build_net(config)
     loss_fns, loss_weights = build_losses(config)
@@ -239,7 +239,10 @@ def build_test(config, device=None):
         raise ValueError("The cuda is not available. Please set the device in the predictor section to 'cpu'.")
     device = torch.device(dev_name)
     test_dataset = build_dataset(config.dataset, 'test')
-    test_loader = get_instance(ns['data'], config.dataloader, test_dataset)
+    dl = Box(config.dataloader.to_dict())
+    dl.kwargs = dl.get('kwargs') or Box()
+    dl.kwargs.update(shard_padding=False)
+    test_loader = get_instance(ns['data'], dl, test_dataset)
     net = build_net(config)
     loss_fns, loss_weights = build_losses(config)
     metric_fns = build_metrics(config)

@@ -251,9 +251,6 @@ static inline bool chunk_ok(const vsrk_tensor5* t, int esize) {
          t->sw % epc == 0 && block_ok && stride_ok;
 }
 
-// bf16 LDS-DMA weight-gradient path (conv_wgrad_fast.hip): 1 = launched the
-// slab kernel, 0 = not eligible (use conv_wgrad_kernel).
-int vsrk_conv_wgrad_fast(const vsrk_conv::WgradArgs& a, int nco, int nci, hipStream_t s);
 // pipelined 16-bit 3x3(x3) weight gradient (conv_wgrad_pipe.hip): 1 = launched the slab kernel, 0 = not eligible.
 int vsrk_conv_wgrad_pipe(const vsrk_conv::WgradArgs& a, int nco, int nci, int dtype, hipStream_t s);
 // thin-channel weight gradient (conv_thin.hip): 1 = launched the slab kernel, 0 = not eligible.

@@ -42,12 +42,10 @@ extern "C" int vsrk_conv_set_path(const char* path, int32_t mode) {
   const std::string p(path);
   if (p == "fast") g_fast_mode = mode;
   else if (p == "thin") vsrk_g_thin_mode = mode;
-  else if (p == "wgrad_fast") vsrk_g_wgrad_fast_mode = mode;
   else if (p == "wgrad_pipe") vsrk_g_wgrad_pipe_mode = mode;
-  else if (p == "k3") vsrk_g_k3_mode = mode;
   else if (p == "pw") vsrk_g_pw_mode = mode;
   else if (p == "roll") vsrk_conv_set_roll_mode(mode);
-  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, k3, pw, roll, thin, wgrad_fast, wgrad_pipe)", path);
+  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, pw, roll, thin, wgrad_pipe)", path);
   return VSRK_OK;
 }
 
@@ -69,7 +67,6 @@ int vsrk_conv_fwd_fast(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   if (g_fast_mode == 0) return 0;
   if (!vsrk_is16(x->dtype)) return 0;
   if (const int rl = vsrk_conv_fwd_roll(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s)) return rl;
-  if (const int k3 = vsrk_conv_fwd_k3(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s)) return k3;
   if (!chunk_ok(x, 2) || x->c % 8 != 0) return 0;
   const int xr = x->shuffle > 1 ? x->shuffle : 1, yr = y->shuffle > 1 ? y->shuffle : 1;
   if (xr > 1 && (x->c / (xr * xr)) % 32 != 0) return 0;

@@ -244,44 +244,70 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[k][m][i] = 0.f;
 
-  // One stage on slot SLOT: the A fragments of all three kw (4 halo rows
-  // each) are read once; then per bank b (kd = the tap whose output depth
-  // lives in bank b) and kw, 3 B fragments and 6 MFMAs, B software-pipelined
-  // one group ahead (read unconditionally: an idle kd's taps are zeros).  The
-  // DMA pieces of the stage two ahead are issued in the first groups.
-  auto compute = [&](auto slot_c, int P, unsigned km, const Dma& dn, bool don) __attribute__((always_inline)) {
+  // BN-affine/ReLU prologue on this lane's own landed A piece q of slot `sl`
+  // (in-image pieces; the halo stays zero as in the reference, which pads
+  // relu(bn(x))): c = the stage's channel chunk, m = its lane mask.
+  const bool relu_in = (a.prologue & VSRK_PRO_RELU) != 0;
+  auto transform_piece = [&](char* sl, int q, int c, unsigned m) __attribute__((always_inline)) {
+    const int j = wave + RNW * q;
+    if (((qa & m) >> q) & 1) {
+      uint4* p = reinterpret_cast<uint4*>(sl + j * 1024 + lane * 16);
+      const int ww = hwv[q] & 0xff;
+      *p = prologue_lds<H>(*p, c * RCH + 8 * ((lane & 1) ^ ((ww >> 3) & 1)), relu_in, lsc, lsh);
+    }
+  };
+
+  // One stage on slot SLOT.  Groups (kw, bank b) in kw-major order: the 4
+  // A fragments (halo rows) of a kw are read one kw ahead, the 3 B fragments
+  // of a group (taps (kd_b, kh, kw); kd_b = the tap whose output depth lives
+  // in bank b) one group ahead, both unconditionally (an idle kd's taps are
+  // zeros), then 6 MFMAs if bank b has work.  Groups 0-5 each issue one DMA
+  // piece of the stage two ahead (slot SLOT+2); groups 6-8 apply the BN/ReLU
+  // prologue to this wave's A pieces of the NEXT stage (slot SLOT+1, landed
+  // one stage ago), beside the MFMAs instead of in front of the barrier.
+  auto compute = [&](auto slot_c, int P, unsigned km, const Dma& dn, bool don, bool tnext, int tc,
+                     unsigned tm) __attribute__((always_inline)) {
     constexpr int SLOT = decltype(slot_c)::value;
     const char* sl = lds + SLOT * RSLOT;
-    uint4 ax[3][RMS + 2];
-#pragma unroll
-    for (int kw = 0; kw < 3; ++kw)
-#pragma unroll
-      for (int hr = 0; hr < RMS + 2; ++hr)
-        ax[kw][hr] = *reinterpret_cast<const uint4*>(sl + abase[kw] + hr * RHW * 32);
+    char* sl1 = lds + ((SLOT + 1) % 3) * RSLOT;
     const int pm = P % 3;
     uint32_t bofs[3];  // byte offset of the taps of the kd whose output depth is in bank b
 #pragma unroll
     for (int b = 0; b < 3; ++b) bofs[b] = (uint32_t)(((pm + 3 - b) % 3) * 9 * 1024);
     const unsigned bm = ((km & 1) ? (1u << pm) : 0u) | ((km & 2) ? (1u << ((pm + 2) % 3)) : 0u) |
                         ((km & 4) ? (1u << ((pm + 1) % 3)) : 0u);  // banks with work
+    uint4 ax[2][RMS + 2];
     uint4 bw[2][3];
+    auto load_a = [&](uint4* af, int kw) __attribute__((always_inline)) {
+#pragma unroll
+      for (int hr = 0; hr < RMS + 2; ++hr) af[hr] = *reinterpret_cast<const uint4*>(sl + abase[kw] + hr * RHW * 32);
+    };
     auto load_b = [&](uint4* bf, int g) __attribute__((always_inline)) {
-      const int b = g / 3, kw = g % 3;
+      const int kw = g / 3, b = g % 3;
       const char* pb = sl + bbase + bofs[b] + kw * 1024;
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) bf[kh] = *reinterpret_cast<const uint4*>(pb + kh * 3 * 1024);
     };
+    load_a(ax[0], 0);
     load_b(bw[0], 0);
 #pragma unroll
     for (int g = 0; g < 9; ++g) {
+      const int kw = g / 3, b = g % 3;
       if (g + 1 < 9) load_b(bw[(g + 1) & 1], g + 1);
+      if (b == 1 && kw + 1 < 3) load_a(ax[(kw + 1) & 1], kw + 1);
       if (g < RNQ && don) dma(dn, g, (SLOT + 2) % 3);
-      const int b = g / 3, kw = g % 3;
+      if constexpr (PRO) {
+        if (g == RNQ && tnext) {
+          if (don) roll_wait_vmcnt<RNQ>();  // the next stage's pieces landed (the one after stays in flight)
+          else roll_wait_vmcnt<0>();
+        }
+        if (g >= RNQ && tnext) transform_piece(sl1, g - RNQ, tc, tm);
+      }
       if ((bm >> b) & 1) {
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-          for (int ms = 0; ms < RMS; ++ms) mma<H>(acc[b][ms], bw[g & 1][kh], ax[kw][ms + kh]);
+          for (int ms = 0; ms < RMS; ++ms) mma<H>(acc[b][ms], bw[g & 1][kh], ax[kw & 1][ms + kh]);
       }
     }
   };
@@ -331,23 +357,6 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       }
     }
   };
-  // BN-affine/ReLU prologue on this lane's own landed A pieces (in-image ones;
-  // the halo stays zero as in the reference, which pads relu(bn(x)))
-  const bool relu_in = (a.prologue & VSRK_PRO_RELU) != 0;
-  auto transform = [&](auto slot_c, int c, unsigned m) __attribute__((always_inline)) {
-    constexpr int SLOT = decltype(slot_c)::value;
-    const int c0 = c * RCH;
-#pragma unroll
-    for (int q = 0; q < RNQ; ++q) {
-      const int j = wave + RNW * q;
-      if (((qa & m) >> q) & 1) {
-        uint4* p = reinterpret_cast<uint4*>(lds + SLOT * RSLOT + j * 1024 + lane * 16);
-        const int ww = hwv[q] & 0xff;
-        *p = prologue_lds<H>(*p, c0 + 8 * ((lane & 1) ^ ((ww >> 3) & 1)), relu_in, lsc, lsh);
-      }
-    }
-  };
-
   // compute walk: tile ct (decoded when the walk enters it), slice cs, chunk cc
   int t = t_lo + jb;
   if (t >= t_hi) return;
@@ -372,16 +381,31 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     for (int q = 0; q < RNQ; ++q) dma(d1, q, 1);
     vn = advance(nx);
   }
+  // the stage after the current one, for the late prologue: exists, chunk, lane mask
+  bool tnext;
+  int tc;
+  unsigned tm;
+  {
+    Walk k1;
+    k1.t = t; k1.sl = 0; k1.c = 0; k1.tl = ct; k1.m = cm;
+    tnext = advance(k1);
+    tc = k1.c;
+    tm = k1.m;
+  }
   __syncthreads();  // bias / prologue tables visible
+  if constexpr (PRO) {  // the first stage: no earlier compute transformed it
+    if (tnext) roll_wait_vmcnt<RNQ>();
+    else roll_wait_vmcnt<0>();
+#pragma unroll
+    for (int q = 0; q < RNQ; ++q) transform_piece(lds, q, 0, cm);
+  }
   RTile ptl = ct;
   int pdi = -1;     // slice whose end is still to be flushed (-1: none)
   bool pall = false;
   // one stage; false when it was the workgroup's last
   auto step = [&](auto slot_c) __attribute__((always_inline)) -> bool {
-    const bool more = cc + 1 < a.nchunk || cs + 1 < ct.nsl || t + gx < t_hi;
-    if (more) roll_wait_vmcnt<RNQ>();  // this stage landed; the next stays in flight
+    if (tnext) roll_wait_vmcnt<RNQ>();  // this stage landed; the next stays in flight
     else roll_wait_vmcnt<0>();
-    if constexpr (PRO) transform(slot_c, cc, cm);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // this slot ready, the previous one free
     if (pdi >= 0) flush(ptl, pdi, pall);
     const int di = ct.di_lo + cs;
@@ -390,7 +414,11 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     dn.wsrc = nullptr;
     dn.use = 0;
     if (vn) dn = prep(nx);
-    compute(slot_c, di + a.pd, kd_mask(ct.z0, ct.z1, di), dn, vn);
+    compute(slot_c, di + a.pd, kd_mask(ct.z0, ct.z1, di), dn, vn, tnext, tc, tm);
+    // the stage after the next one is nx's (issued just now): it becomes "next"
+    tnext = vn;
+    tc = nx.c;
+    tm = nx.m;
     if (vn) vn = advance(nx);
     // advance the compute walk; a finished slice is flushed after the next barrier
     pdi = -1;

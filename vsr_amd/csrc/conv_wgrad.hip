@@ -458,8 +458,6 @@ extern "C" int vsrk_conv_wgrad(const vsrk_conv_desc* d, const vsrk_tensor5* x, c
     // thin-channel kernel (conv_thin.hip), same slab layout
   } else if (vsrk_is16(x->dtype) && vsrk_conv_wgrad_pipe(a, p.nco, p.nci, x->dtype, s)) {
     // two-stage pipelined kernel (conv_wgrad_pipe.hip), same slab layout
-  } else if (x->dtype == VSRK_BF16 && vec && vsrk_conv_wgrad_fast(a, p.nco, p.nci, s)) {
-    // LDS-DMA kernel (conv_wgrad_fast.hip), same slab layout
   } else if (vsrk_is16(x->dtype)) {
     vsrk_dispatch16(x->dtype, [&](auto tag) {
       using H = decltype(tag);

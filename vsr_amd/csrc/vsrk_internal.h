@@ -21,11 +21,6 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                        const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
 
-// second-generation 3x3(x3) bf16 conv (conv_k3.hip); same return convention
-int vsrk_conv_fwd_k3(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
-                     const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
-                     const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
-
 // rolling-depth 16-bit Conv3d 3x3x3 (conv_roll.hip): forward / data gradient;
 // same return convention; vsrk_conv_set_roll_mode: -1 env VSRK_CONV_ROLL, 0 off, 1 on
 int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
@@ -45,9 +40,7 @@ int vsrk_conv_wgrad_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsr
 
 // path switches (vsrk_conv_set_path): -1 = from the environment, 0 off, 1 on
 extern int vsrk_g_pw_mode;
-extern int vsrk_g_k3_mode;
 extern int vsrk_g_thin_mode;
-extern int vsrk_g_wgrad_fast_mode;
 extern int vsrk_g_wgrad_pipe_mode;
 // vsrk_conv_set_grid_cap: > 0 caps the workgroups of the persistent conv grids
 // and of the weight-gradient split (tests drive the multi-tile loops with it)

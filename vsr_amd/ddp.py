@@ -85,9 +85,16 @@ class GradSync:
         unscale = getattr(self.net, "_grad_unscale", 1.0)  # fp16 loss scale (BaseNet._loss_scale)
         for b, h in enumerate(self._handles):
             self._handles[b].wait()
-            f = unscale if self._avg else unscale / self.world
-            if f != 1.0:
-                self.flat[b].mul_(f)
+        f = unscale if self._avg else unscale / self.world
+        if unscale != 1.0:
+            # fp16: unscale and flag inf / NaN in one pass over the buckets; an
+            # overflow on any rank reaches every rank through the all-reduce,
+            # so every rank skips the same step (BaseNet.step_ok)
+            from .nets.base_net import unscale_check
+            self.net._found_inf = unscale_check(self.flat, f)
+        elif f != 1.0:
+            for buf in self.flat:
+                buf.mul_(f)
         self._reset()
         self._attach()
 
@@ -106,18 +113,25 @@ class SyncBNAllReduce:
 
     ``hook(sums)`` sums the per-channel (sum, sumsq) -- or, in backward,
     (sum_dy, sum_dy_xhat) -- over every rank in place (one small all-reduce
-    per BN layer, at most 2 x 256 floats) and returns the factor from the
-    local to the global voxel count.  Ranks hold equal-shaped shards (the
-    DistributedSampler pads the dataset to a multiple of the world size), so
-    that factor is the world size and no host sync is needed."""
+    per BN layer, at most 2 x 256 floats).  The global voxel count of a layer
+    is its depth times the sum over ranks of N*H*W of the step's input
+    (ranks may hold batches of different sizes: uncropped slices, a last
+    partial batch): ``global_count(local)`` all-reduces that once per forward
+    (one host read per step), and the net scales every layer's count by it."""
 
     def __init__(self, group=None):
         self.group = group
         self.world = dist.get_world_size(group)
 
-    def __call__(self, t: torch.Tensor) -> int:
+    def __call__(self, t: torch.Tensor) -> None:
         dist.all_reduce(t, group=self.group)
-        return self.world
+
+    def global_count(self, local: int) -> int:
+        """Sum of `local` over the ranks (exact in float64 up to 2^53)."""
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(self.group) == "nccl" else "cpu"
+        t = torch.tensor([float(local)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, group=self.group)
+        return int(t.item())
 
 
 def enable_sync_bn(net, group=None) -> bool:

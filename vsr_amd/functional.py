@@ -206,7 +206,7 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, k, pad, dw: torch.Tensor, dbia
 
 
 def set_conv_path(path: str, mode: int) -> None:
-    """Select a conv kernel family ("fast", "thin", "wgrad_fast"): -1 default, 0 off, 1 on."""
+    """Select a conv kernel family ("fast", "pw", "roll", "thin", "wgrad_pipe"): -1 default, 0 off, 1 on."""
     N.check(_lib().vsrk_conv_set_path(path.encode(), int(mode)), "conv_set_path")
 
 

@@ -34,8 +34,12 @@ class BaseNet(nn.Module):
         super().__init__()
         self.compute_dtype = torch.bfloat16
         self._grad_sink = None  # vsr_amd.ddp.GradSync when data-parallel
-        # fp16 loss scale: None = automatic (see _loss_scale), else a fixed float
+        # fp16 loss scale: None = dynamic (see _loss_scale / step_ok), else a fixed float
         self.loss_scale = None
+        self._scale = None       # current dynamic fp16 scale (set at the first fp16 backward)
+        self._good_steps = 0     # finite steps since the last change of _scale
+        self.scale_growth_interval = 2000
+        self._found_inf = None   # device flag: the last fp16 backward produced an inf/NaN gradient
         # weight gradients on a second stream, overlapped with the data-gradient
         # chain: per net class (_OVERLAP_WGRAD), VSR_OVERLAP_WGRAD=0/1 overrides
         env = os.environ.get("VSR_OVERLAP_WGRAD")
@@ -110,25 +114,54 @@ class BaseNet(nn.Module):
         the factor instead."""
         self.compute_dtype = _COMPUTE_DTYPES[precision]
         self.loss_scale = loss_scale
+        self._scale = None
+        self._good_steps = 0
+        self._found_inf = None
         return self
 
     def _loss_scale(self, grads) -> float:
         """Factor the output gradient is multiplied by before an fp16 backward
-        (and every parameter gradient divided by after it) -- the static
-        counterpart of torch.cuda.amp.GradScaler.  The reference's losses are
-        means over the output (losses.py:5-34, nn.L1Loss/MSELoss), so the
-        output gradient is O(1/N) for N output elements: below fp16's normal
-        range (6.1e-5) at N > 16k, and the data gradients of early layers sit
-        further down in fp16's subnormals, where fewer significant bits remain.
-        Automatic scale: 2^floor(log2 N), i.e. output gradients in [1, 2).  bf16
-        / fp32: 1."""
+        (and every parameter gradient divided by after it), as
+        torch.cuda.amp.GradScaler does.  The reference's losses are means over
+        the output (losses.py:5-34, nn.L1Loss/MSELoss), so the output gradient
+        is O(1/N) for N output elements: below fp16's normal range (6.1e-5) at
+        N > 16k, and the data gradients of early layers sit further down in
+        fp16's subnormals, where fewer significant bits remain.  The dynamic
+        scale starts at 2^floor(log2 N) (output gradients in [1, 2)); step_ok()
+        halves it after an overflow and doubles it after
+        scale_growth_interval finite steps.  bf16 / fp32: 1."""
         if self.compute_dtype != torch.float16:
             return 1.0
         if self.loss_scale is not None:
             return float(self.loss_scale)
-        gs = grads if isinstance(grads, (tuple, list)) else (grads,)
-        n = sum(g.numel() for g in gs if g is not None)
-        return float(2 ** max(0, max(n, 1).bit_length() - 1))
+        if self._scale is None:
+            gs = grads if isinstance(grads, (tuple, list)) else (grads,)
+            n = sum(g.numel() for g in gs if g is not None)
+            self._scale = float(2 ** max(0, max(n, 1).bit_length() - 1))
+        return self._scale
+
+    def step_ok(self) -> bool:
+        """GradScaler.step/update for the fp16 path: False when the last
+        backward produced an inf or NaN gradient (the caller then skips
+        optimizer.step(), so Adam's state never sees it), and the dynamic scale
+        backs off by half; after scale_growth_interval finite steps it grows by
+        2.  One host read of a device flag per fp16 step; True without one
+        (bf16 / fp32, or no backward since the last call)."""
+        f = self._found_inf
+        if f is None:
+            return True
+        self._found_inf = None
+        found = bool(f.item())
+        if self.loss_scale is None and self._scale is not None:
+            if found:
+                self._scale = max(self._scale * 0.5, 1.0)
+                self._good_steps = 0
+            else:
+                self._good_steps += 1
+                if self._good_steps >= self.scale_growth_interval:
+                    self._scale *= 2.0
+                    self._good_steps = 0
+        return not found
 
     def __repr__(self):
         n = sum(p.numel() for p in self.parameters() if p.requires_grad)
@@ -156,6 +189,17 @@ class BaseNet(nn.Module):
         return False
 
 
+def unscale_check(tensors, inv_scale: float) -> torch.Tensor:
+    """t *= inv_scale for every fp32 tensor; returns a device flag (float32 [1])
+    that is nonzero when any element was inf or NaN (torch's GradScaler
+    kernel, _amp_foreach_non_finite_check_and_unscale_)."""
+    dev = tensors[0].device
+    found = torch.zeros(1, dtype=torch.float32, device=dev)
+    inv = torch.full((1,), inv_scale, dtype=torch.float32, device=dev)
+    torch._amp_foreach_non_finite_check_and_unscale_(tensors, found, inv)
+    return found
+
+
 class _TapeFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, net, inputs, *params):
@@ -179,6 +223,7 @@ class _TapeFunction(torch.autograd.Function):
         net._join_wgrad()
         ctx.tape = None
         if scale != 1.0 and net._grad_sink is None:
-            for t in g.values():
-                t.mul_(1.0 / scale)  # the data-parallel path unscales in GradSync.finish
+            # unscale every parameter gradient and flag any inf / NaN (one fused
+            # pass; the data-parallel path does this on its buckets in GradSync.finish)
+            net._found_inf = unscale_check([t for t in g.values()], 1.0 / scale)
         return (None, None, *[g.get(id(p)) for p in ctx.params])

@@ -108,7 +108,8 @@ class DUFNet(BaseNet):
             sums = sums.clone()  # the SyncBN hook all-reduces in place
         count = x.shape[0] * x.shape[1] * x.shape[2] * x.shape[3]
         if self.bn_allreduce is not None:
-            count *= self.bn_allreduce(sums)
+            self.bn_allreduce(sums)
+            count = x.shape[1] * self._global_nhw  # depth x the N*H*W of every rank
         st = F.bn_finalize(sums, count, bn.weight, bn.bias, bn.eps, bn.momentum if bn.momentum is not None else 0.1,
                            bn.running_mean if bn.track_running_stats else None,
                            bn.running_var if bn.track_running_stats else None)
@@ -155,6 +156,8 @@ class DUFNet(BaseNet):
         if T - 2 * 3 != 1:
             # the reference's residual branch squeezes depth 1 (duf_net.py:94-96) and only works for T = 7
             raise RuntimeError(f"DUFNet needs num_frames = 7 (got {T}): depth after the dense layer must be 1")
+        if self.training and self.bn_allreduce is not None:
+            self._global_nhw = self.bn_allreduce.global_count(n * h * w)  # SyncBN: the global batch
         frames = torch.stack(inputs, dim=2)  # (n, cin, T, h, w) fp32
         xv = F.to_view(frames, cd, cpad=8)[..., :cin]  # (n, T, h, w, cin), chunk-aligned storage
         C = torch.empty((n, T, h, w, ctot), dtype=cd, device=dev)

@@ -7,9 +7,19 @@ the network in eval mode, per-frame losses and metrics on the HIP kernels
 log keys, and -- with ``exported=True`` -- the results CSV (one row per
 frame: name, metrics, losses), a PNG per SR frame and a GIF per sequence.
 
+Export names follow the reference exactly: the patient / sequence / frame
+ids are parsed from the dataset's file names (SISR ``<patient>_2d_<slice>_<frame>``,
+MISR / VSR ``<patient>_2d+1d_<sequence>`` with the frame index t of the
+sample), images are ``imgs/<patient>/<slice>_<frame>.png`` and one GIF per
+sequence ``videos/<patient>/<sequence>.gif`` (SISR / MISR collect the frames
+of a sequence and write its GIF when the sequence id changes).
+
 Differences: images are written with PIL (the reference's scipy.misc.imsave
 was removed from SciPy and imageio is not a dependency here); checkpoints
-load with ``weights_only=True``.
+load with ``weights_only=True`` (a reference checkpoint's pickled Monitor
+resolves through the same allow-list as the trainer's); the SISR / MISR
+predictors also write the GIF of the LAST sequence, which the reference's
+loop never flushes (acdc_sisr_predictor.py:72-79 only writes on a change).
 """
 from __future__ import annotations
 
@@ -21,6 +31,7 @@ import numpy as np
 import torch
 
 from .. import metrics as M
+from ..callbacks.monitor import safe_globals
 from ..utils import denormalize
 from .trainers import _metric
 
@@ -65,7 +76,8 @@ class BasePredictor:
 
     def load(self, path):
         """base_predictor.py:130-136 (net state only), without unpickling code."""
-        ckpt = torch.load(path, map_location=self.device, weights_only=True)
+        with torch.serialization.safe_globals(safe_globals()):
+            ckpt = torch.load(path, map_location=self.device, weights_only=True)
         self.net.load_state_dict(ckpt["net"])
 
     # -- per-frame pieces (shared by the SISR / MISR / VSR predictors) ----------
@@ -88,15 +100,17 @@ class BasePredictor:
         return torch.stack(rows, dim=1)
 
     def _sample_name(self, index):
-        """Patient and sequence id from the dataset's file names (acdc_vsr_predictor.py:55-58)."""
+        """(filename, patient, sequence id, frame id or None) of sample `index`
+        from the dataset's file names (acdc_vsr_predictor.py:55-58,
+        acdc_misr_predictor.py:56-59,68, acdc_sisr_predictor.py:56-58)."""
         data = getattr(self.test_dataloader.dataset, "data", None)
-        if data is None:
-            return f"sample{int(index)}", "patient", f"sequence{int(index)}"
-        lr_path = Path(data[int(index)][0])
-        filename = lr_path.parts[-1].split(".")[0]
+        if data is None:  # a dataset without file names (synthetic)
+            return f"sample_2d+1d_sequence{int(index):02d}", "sample", f"sequence{int(index):02d}", "frame01"
+        entry = data[int(index)]
+        filename = Path(entry[0]).parts[-1].split(".")[0]
         parts = filename.split("_")
-        patient, sid = parts[0], parts[-1]
-        return filename, patient, sid
+        fid = f"frame{int(entry[2]) + 1:0>2d}" if len(entry) > 2 else "frame01"  # MISR: the window's target frame
+        return filename, parts[0], parts[2], fid
 
     def _to_uint8(self, x):
         return denormalize(x, self.dataset_name).squeeze().detach().cpu().numpy().astype(np.uint8)
@@ -113,6 +127,40 @@ class BasePredictor:
         frames = [Image.fromarray(i) for i in imgs]
         frames[0].save(path, save_all=True, append_images=frames[1:], loop=0)
 
+    # -- export (results rows, PNG per SR frame, GIF per sequence) ---------------
+    def _dirs(self, patient):
+        vdir, idir = self.saved_dir / "videos" / patient, self.saved_dir / "imgs" / patient
+        vdir.mkdir(parents=True, exist_ok=True)
+        idir.mkdir(parents=True, exist_ok=True)
+        return vdir, idir
+
+    def _flush_video(self, state):
+        """GIF of the collected frames of the current sequence (SISR / MISR)."""
+        if state["sr_imgs"]:
+            vdir, _ = self._dirs(state["patient"])
+            self._dump_video(vdir / f"{self._video_name(state['sid'])}.gif", state["sr_imgs"])
+            state["sr_imgs"] = []
+
+    def _video_name(self, sid):
+        return sid
+
+    @staticmethod
+    def _row_name(filename, fid):
+        return filename.replace("2d+1d", "2d").replace("sequence", "slice") + f"_{fid}"
+
+    def _export(self, state, results, filename, patient, sid, fid, outs, metrics, losses):
+        """One sample holding frame `fid` of sequence `sid` (SISR / MISR: a
+        frame; acdc_misr_predictor.py:66-91, acdc_sisr_predictor.py:66-90)."""
+        row = torch.cat([metrics, losses], dim=1)[0].cpu().tolist()
+        results.append([self._row_name(filename, fid), *row])
+        if sid != state["sid"]:
+            self._flush_video(state)
+        img = self._to_uint8(outs[0])
+        state["sr_imgs"].append(img)
+        state["sid"], state["patient"] = sid, patient
+        _, idir = self._dirs(patient)
+        self._save_png(idir / (sid.replace("sequence", "slice") + f"_{fid}.png"), img)
+
     # -- the loop ---------------------------------------------------------------
     def _get_inputs_targets(self, batch):
         raise NotImplementedError
@@ -126,13 +174,14 @@ class BasePredictor:
         header = (["name"] + [fn.__class__.__name__ for fn in self.metric_fns] +
                   [fn.__class__.__name__ for fn in self.loss_fns])
         results = [header]
+        state = {"sr_imgs": [], "sid": None, "patient": None}
         log = self._init_log()
         count = 0
         for batch in self.test_dataloader:
             batch = self._allocate_data(batch)
             inputs, targets, index = self._get_inputs_targets(batch)
             with torch.no_grad():
-                filename, patient, sid = self._sample_name(index)
+                filename, patient, sid, fid = self._sample_name(index)
                 outputs = self.net(inputs)
                 outs, tgts = self._frames_of(outputs, targets)
                 losses = self._frame_losses(outs, tgts)                  # (T, L)
@@ -140,18 +189,7 @@ class BasePredictor:
                 metrics = self._frame_metrics(outs, tgts, patient)      # (T, M)
             T = len(outs)
             if self.exported:
-                rows = torch.cat([metrics, losses], dim=1).cpu().tolist()
-                stem = filename.replace("2d+1d", "2d").replace("sequence", "slice")
-                for t, row in enumerate(rows):
-                    results.append([stem + f"_frame{t + 1:0>2d}", *row])
-                imgs = [self._to_uint8(o) for o in outs]
-                vdir = self.saved_dir / "videos" / patient
-                idir = self.saved_dir / "imgs" / patient
-                vdir.mkdir(parents=True, exist_ok=True)
-                idir.mkdir(parents=True, exist_ok=True)
-                self._dump_video(vdir / f"{sid}.gif", imgs)
-                for t, img in enumerate(imgs):
-                    self._save_png(idir / (sid.replace("sequence", "slice") + f"_frame{t + 1:0>2d}.png"), img)
+                self._export(state, results, filename, patient, sid, fid, outs, metrics, losses)
             # acdc_vsr_predictor.py:160-170: frame-weighted
             log["Loss"] += loss.item() * T
             for fn, v in zip(self.loss_fns, losses.mean(dim=0)):
@@ -160,6 +198,7 @@ class BasePredictor:
                 log[fn.__class__.__name__] += v.item() * T
             count += T
         if self.exported:
+            self._flush_video(state)
             self.saved_dir.mkdir(parents=True, exist_ok=True)
             with open(self.saved_dir / "results.csv", "w", newline="") as fh:
                 csv.writer(fh).writerows(results)
@@ -178,6 +217,18 @@ class AcdcVSRPredictor(BasePredictor):
     def _frames_of(self, outputs, targets):
         return list(outputs), list(targets)
 
+    def _export(self, state, results, filename, patient, sid, fid, outs, metrics, losses):
+        """A whole sequence (acdc_vsr_predictor.py:66-96): one row, one PNG per
+        frame, the sequence's GIF."""
+        stem = filename.replace("2d+1d", "2d").replace("sequence", "slice")
+        for t, row in enumerate(torch.cat([metrics, losses], dim=1).cpu().tolist()):
+            results.append([stem + f"_frame{t + 1:0>2d}", *row])
+        imgs = [self._to_uint8(o) for o in outs]
+        vdir, idir = self._dirs(patient)
+        self._dump_video(vdir / f"{sid}.gif", imgs)
+        for t, img in enumerate(imgs):
+            self._save_png(idir / (sid.replace("sequence", "slice") + f"_frame{t + 1:0>2d}.png"), img)
+
 
 class Dsb15VSRPredictor(AcdcVSRPredictor):
     dataset_name = "dsb15"
@@ -185,6 +236,10 @@ class Dsb15VSRPredictor(AcdcVSRPredictor):
 
 class AcdcMISRPredictor(BasePredictor):
     """acdc_misr_predictor.py: T LR frames -> the centre SR frame."""
+
+    @staticmethod
+    def _row_name(filename, fid):
+        return filename.replace("2d+1d", "2d").replace("sequence", "slice") + f"_{fid}"
 
     def _get_inputs_targets(self, batch):
         return batch["lr_imgs"], batch["hr_img"], batch["index"]
@@ -199,6 +254,19 @@ class Dsb15MISRPredictor(AcdcMISRPredictor):
 
 class AcdcSISRPredictor(BasePredictor):
     """acdc_sisr_predictor.py: one LR slice -> one SR slice."""
+
+    def _sample_name(self, index):
+        """<patient>_2d_<slice>_<frame> (acdc_sisr_predictor.py:56-58)."""
+        filename, patient, sid, _ = super()._sample_name(index)
+        parts = filename.split("_")
+        return filename, patient, sid, parts[3] if len(parts) > 3 else "frame01"
+
+    @staticmethod
+    def _row_name(filename, fid):
+        return filename
+
+    def _video_name(self, sid):
+        return sid.replace("slice", "sequence")
 
     def _get_inputs_targets(self, batch):
         return batch["lr_img"], batch["hr_img"], batch["index"]

@@ -153,7 +153,9 @@ class BaseTrainer:
                 loss.backward()
                 if self.grad_sync is not None:
                     self.grad_sync.finish()
-                self.optimizer.step()
+                # fp16: skip the update of a step whose gradients overflowed (GradScaler)
+                if getattr(self.net, "step_ok", None) is None or self.net.step_ok():
+                    self.optimizer.step()
             else:
                 with torch.no_grad():
                     outputs = self.net(inputs)
