@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Throughput benchmark of the cardiac cine-MRI SR train step on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--models edsr,duf] [--config cfg2|cfg3|cfg5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--models edsr,duf] [--config cfg2|cfg3|cfg4|cfg5]
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver, N > 1)
 
 With --gpus N > 1 and no torchrun environment, bench.py starts the N ranks
@@ -30,7 +30,13 @@ roofline: the model's dominant conv, forward + data gradient + weight
           3x3 64->64; DUF: the six Conv3d 3x3x3 F->32 (F = 64..224).
 --config picks the BASELINE.json workload: cfg2 (default: ACDC, 4 x 16 x
 128 x 128 per GPU, bf16, EDSR + DUF), cfg3 (DSB15, DRF on 4 x 30-frame
-stacks), cfg5 (ACDC + DSB15 mixed, fp16, batch 8 per GPU, EDSR + DUF).
+stacks), cfg4 (ACDC full volumes: DUF on 2 uncropped 30-frame cine
+volumes of 64 x 64 LR / 256 x 256 HR per GPU), cfg5 (ACDC + DSB15 mixed,
+fp16, batch 8 per GPU, EDSR + DUF).
+comm (N > 1): the data-parallel traffic of one step -- gradient bytes and
+          buckets, and the time of the step's bucket all-reduces and SyncBN
+          all-reduces each run alone after the timed region (HIP events), to
+          set beside ms_per_step: what the overlap with backward must hide.
 measured_peak: this device's dense bf16 MFMA rate and HBM copy rate from
           two microbenchmarks (vsrk_peak_mfma / vsrk_peak_copy), with each
           roofline's fraction of the measured MFMA rate beside the vendor one.
@@ -71,6 +77,8 @@ CONFIGS = {
                  desc="ACDC 4x SR, 3D 16x128x128 volumes bf16, batch 4 per GPU"),
     "cfg3": dict(B=4, T=30, dataset="dsb15", precision="bf16", models="drf",
                  desc="DSB15 cine 4x SR, T=30 2D+t stacks (DRF), batch 4 per GPU"),
+    "cfg4": dict(B=2, T=30, H=64, W=64, dataset="acdc", precision="bf16", models="duf",
+                 desc="ACDC 4x SR, full 3D cine volumes (2 x 30 frames of 64x64 LR, 256x256 HR, no crop) per GPU"),
     "cfg5": dict(B=8, T=16, dataset="mixed", precision="fp16", models="edsr,duf",
                  desc="mixed ACDC+DSB15 4x SR, fp16 MFMA path, batch 8 per GPU"),
 }
@@ -213,6 +221,39 @@ def cpu_baseline(model, budget_s=20.0):
             "sample": f"{sample}; median of {len(times)} steps after 1 warm-up ({med:.2f} s/step)"}
 
 
+def comm_report(net, sync, dev, iters=20):
+    """The step's collectives, each timed alone (after the timed region): the
+    gradient bucket all-reduces of GradSync and the SyncBN all-reduces (one per
+    BatchNorm per direction, 2 x C floats)."""
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / iters
+
+    def buckets():
+        for b in range(len(sync.flat)):
+            sync._launch(b)
+        for h in sync._handles:
+            h.wait()
+        sync._reset()
+
+    out = {"grad_bytes": int(sum(f.numel() * 4 for f in sync.flat)), "buckets": len(sync.flat),
+           "grad_allreduce_ms": timed(buckets)}
+    bns = [m for m in net.modules() if isinstance(m, torch.nn.BatchNorm3d)]
+    if bns and getattr(net, "bn_allreduce", None) is not None:
+        ts = [torch.zeros(2 * m.num_features, device=dev) for m in bns]
+        out["syncbn_allreduces_per_step"] = 2 * len(bns)
+        out["syncbn_allreduce_ms_per_step"] = 2 * timed(lambda: [dist.all_reduce(t) for t in ts])
+    return out
+
+
 def run_model(name, args, world, rank, dev):
     spec = MODELS[name]
     torch.manual_seed(0)  # identical initial weights on every rank
@@ -291,6 +332,7 @@ def run_model(name, args, world, rank, dev):
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+    comm = comm_report(net, sync, dev) if world > 1 else None
     vox_step = B * T * H * W
     peak = PEAK[args.precision]
     achieved = flop / kernel_s if kernel_s > 0 else None
@@ -310,6 +352,8 @@ def run_model(name, args, world, rank, dev):
         "final_loss": float(loss.item()),
         "graph": graph,
     }
+    if comm is not None:
+        res["comm"] = comm
     del net, opt, sync
     torch.cuda.empty_cache()
     return res
@@ -362,9 +406,10 @@ def worker(args, world, rank, local):
 def apply_config(args):
     """Set the module-level workload of --config (also in spawned ranks, which
     re-import this module with the cfg-2 defaults)."""
-    global B, T, DATASET
+    global B, T, H, W, DATASET
     cfg = CONFIGS[args.config]
     B, T, DATASET = cfg["B"], cfg["T"], cfg["dataset"]
+    H, W = cfg.get("H", 128), cfg.get("W", 128)
 
 
 def _spawned(local, args, world, port):

@@ -19,7 +19,11 @@ from . import make_golden as mg
 
 
 def main():
+    import os
+    only = os.environ.get("GOLDEN_ONLY")
     for name, spec in mg.CASES.items():
+        if only and name not in only.split(","):
+            continue
         path = mg.OUT / f"{name}.pt"
         fx = torch.load(path, weights_only=True)
         _, _, cls, kwargs, _, _ = spec

@@ -33,7 +33,7 @@ CASES = {
                       "sisr", (2, 1, 10, 9)),
     "edsr_x2_cfg1": ("src.model.nets.edsr_net", "EDSRNet", cpu_nets.EDSRRef,
                      dict(in_channels=1, out_channels=1, num_resblocks=16, num_features=64, upscale_factor=2),
-                     "sisr", (2, 1, 16, 16)),
+                     "sisr", (2, 1, 64, 64)),  # BASELINE cfg 1: 64x64 LR slices, batch 2
     "edsr_x4_canon": ("src.model.nets.edsr_net", "EDSRNet", cpu_nets.EDSRRef,
                       dict(in_channels=1, out_channels=1, num_resblocks=16, num_features=64, upscale_factor=4),
                       "sisr", (2, 1, 12, 16)),

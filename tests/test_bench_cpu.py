@@ -11,18 +11,23 @@ spec.loader.exec_module(bench)
 
 
 def test_configs_cover_the_one_node_baseline_configs():
-    assert set(bench.CONFIGS) == {"cfg2", "cfg3", "cfg5"}
+    assert set(bench.CONFIGS) == {"cfg2", "cfg3", "cfg4", "cfg5"}
     assert bench.CONFIGS["cfg2"]["B"] * bench.CONFIGS["cfg2"]["T"] * 128 * 128 == 1048576
     assert bench.CONFIGS["cfg5"]["precision"] == "fp16" and bench.CONFIGS["cfg5"]["B"] == 8
     assert bench.CONFIGS["cfg3"]["T"] == 30 and bench.CONFIGS["cfg3"]["models"] == "drf"
+    # cfg 4: DUF on whole (uncropped) ACDC cine volumes: 256 x 256 HR at 4x
+    c4 = bench.CONFIGS["cfg4"]
+    assert c4["models"] == "duf" and c4["H"] * 4 == 256 and c4["W"] * 4 == 256 and c4["T"] == 30
 
 
 def test_apply_config_sets_the_workload():
     args = argparse.Namespace(config="cfg3")
     bench.apply_config(args)
     assert (bench.B, bench.T, bench.DATASET) == (4, 30, "dsb15")
+    bench.apply_config(argparse.Namespace(config="cfg4"))
+    assert (bench.B, bench.T, bench.H, bench.W) == (2, 30, 64, 64)
     bench.apply_config(argparse.Namespace(config="cfg2"))
-    assert (bench.B, bench.T, bench.DATASET) == (4, 16, "acdc")
+    assert (bench.B, bench.T, bench.DATASET, bench.H, bench.W) == (4, 16, "acdc", 128, 128)
 
 
 class _V:

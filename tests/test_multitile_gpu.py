@@ -228,6 +228,7 @@ def test_wgrad_pipe_matches_generic(case, dtype):
 
     def run(pipe, cap):
         F.set_conv_path("wgrad_pipe", pipe)
+        F.set_conv_path("wgrad_roll", 0)  # the rolling 3x3x3 kernel has its own tests (test_wgrad_roll_gpu.py)
         F.set_grid_cap(cap)
         try:
             dw = torch.empty((co, ci, *k), dtype=torch.float32, device=DEV)
@@ -236,6 +237,7 @@ def test_wgrad_pipe_matches_generic(case, dtype):
             return dw.cpu(), (db.cpu() if bias else None)
         finally:
             F.set_conv_path("wgrad_pipe", -1)
+            F.set_conv_path("wgrad_roll", -1)
             F.set_grid_cap(0)
 
     xin = _q(x, dtype)

@@ -97,7 +97,7 @@ def test_export_names_follow_the_reference(kind, tmp_path):
     from vsr_amd.callbacks.monitor import Monitor
     from vsr_amd.data import AcdcMISRDataset, AcdcSISRDataset
 
-    T = 4
+    T = 8  # >= num_frames: a 7-frame window wraps at most once (acdc_misr_dataset.py:61-68)
     root = make_tree(tmp_path / "data", T=T, H=16, W=16, patients=2)
     tf = [{"name": "Normalize", "kwargs": {"means": [54.089], "stds": [48.084]}}, {"name": "ToTensor"}]
     if kind == "sisr":
@@ -111,7 +111,7 @@ def test_export_names_follow_the_reference(kind, tmp_path):
     net = net.to(DEV).set_precision("fp32")
     # a checkpoint in the reference's format: the Monitor pickled under src.callbacks.monitor
     mod = types.ModuleType("src.callbacks.monitor")
-    mod.Monitor = type("Monitor", (), {})
+    mod.Monitor = type("Monitor", (), {"__module__": "src.callbacks.monitor"})
     for name in ("src", "src.callbacks"):
         sys.modules.setdefault(name, types.ModuleType(name))
     sys.modules["src.callbacks.monitor"] = mod

@@ -137,3 +137,80 @@ def test_roll_data_gradient_duf_unit():
            (2, 1, 1))
     err = (dx.double().cpu() - xr.grad).abs().max().item()
     assert err <= _tol(torch.bfloat16, xr.grad), err
+
+
+# ---- the 2-D form: 3x3 over depth-1 slices, 64-channel output blocks ----
+# (N, D, H, W, Cin, Cout): EDSR body shapes with partial tiles, several
+# samples, a (1,3,3) conv over a 3-slice volume, 128 output channels
+CASES2D = [
+    (3, 1, 20, 40, 64, 64),
+    (2, 1, 16, 32, 32, 64),
+    (1, 3, 9, 35, 64, 128),
+    (2, 1, 33, 70, 64, 64),
+]
+EPI = ["plain", "relu", "res", "mask", "res_acc"]
+
+
+def _run2d(case, dtype, epi, cap=0, roll=-1, seed=0):
+    n, d, h, w, ci, co = case
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn((n, d, h, w, ci), generator=g)
+    wt = torch.randn((co, ci, 1, 3, 3), generator=g) / (9 * ci) ** 0.5
+    b = torch.randn(co, generator=g)
+    res = torch.randn((n, d, h, w, co), generator=g)
+    msk = torch.randn((n, d, h, w, co), generator=g)
+    old = torch.randn((n, d, h, w, co), generator=g)
+    scale = 0.5 if epi in ("res", "mask") else 1.0
+    ref = _ref(_q(x, dtype), _q(wt, dtype), b.double(), (0, 1, 1)) * scale
+    if epi == "relu":
+        ref = torch.relu(ref)
+    if epi == "mask":
+        ref = ref * (_q(msk, dtype) > 0)
+    if epi in ("res", "res_acc"):
+        ref = ref + _q(res, dtype)
+    if epi == "res_acc":
+        ref = ref + _q(old, dtype)
+    y = old.to(DEV, dtype) if epi == "res_acc" else torch.full((n, d, h, w, co), 7.0, dtype=dtype, device=DEV)
+    kw = dict(bias=b.to(DEV), out_scale=scale)
+    if epi == "relu":
+        kw["act"] = F.ACT_RELU
+    if epi == "mask":
+        kw["mask"] = msk.to(DEV, dtype)
+    if epi in ("res", "res_acc"):
+        kw["residual"] = res.to(DEV, dtype)
+    if epi == "res_acc":
+        kw["accumulate"] = True
+    F.set_grid_cap(cap)
+    F.set_conv_path("roll", roll)
+    try:
+        F.conv(x.to(DEV, dtype), F.pack_weight(wt.to(DEV), 0, dtype), y, (1, 3, 3), (0, 1, 1), **kw)
+    finally:
+        F.set_grid_cap(0)
+        F.set_conv_path("roll", -1)
+    torch.cuda.synchronize()
+    return y.double().cpu(), ref
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("epi", EPI)
+@pytest.mark.parametrize("case", CASES2D)
+def test_roll_2d(case, epi, dtype):
+    y, ref = _run2d(case, dtype, epi)
+    err = (y - ref).abs().max().item()
+    assert err <= _tol(dtype, ref), err
+
+
+@pytest.mark.parametrize("epi", EPI)
+def test_roll_2d_tiling_invariant_and_path(epi):
+    """a capped grid (many tiles per workgroup: the operand prefetch and the
+    DMA walk cross tiles) gives bitwise the default output; the conv_fast
+    path agrees within rounding and is a different kernel"""
+    case = (2, 1, 33, 70, 64, 64)
+    y0, ref = _run2d(case, torch.bfloat16, epi)
+    for cap in (1, 3, 7):
+        y, _ = _run2d(case, torch.bfloat16, epi, cap=cap)
+        assert torch.equal(y, y0), (cap, (y - y0).abs().max().item())
+    yf, _ = _run2d(case, torch.bfloat16, epi, roll=0)
+    tol = _tol(torch.bfloat16, ref)
+    assert (yf - ref).abs().max().item() <= tol
+    assert (y0 - ref).abs().max().item() <= tol

@@ -77,6 +77,9 @@ def main():
         "fwd": lambda: F.conv(x, wp, y, k, pad, bias=b),
         "fwdpro": lambda: F.conv(x, wp, y, k, pad, bias=b, prologue=F.PRO_AFFINE_RELU, pro_scale=psc, pro_shift=psh),
         "res": lambda: F.conv(x, wp, y, k, pad, bias=b, out_scale=0.1, residual=res),
+        "relu": lambda: F.conv(x, wp, y, k, pad, bias=b, act=F.ACT_RELU),
+        "mask": lambda: F.conv(gy, wp1, dx, k, dpad, out_scale=0.1, mask=x),
+        "resacc": lambda: F.conv(gy, wp1, dx, k, dpad, residual=x, accumulate=True),
         "wgrad": lambda: F.conv_wgrad(x, gy, k, pad, dw, db),
         "wgradpro": lambda: F.conv_wgrad(x, gy, k, pad, dw, db, prologue=F.PRO_AFFINE_RELU, pro_scale=psc,
                                          pro_shift=psh),

@@ -1,0 +1,43 @@
+# Round 3: new-kernel parity (rolling wgrad, 2-D rolling conv), DUF/EDSR conv microbench A/B,
+# bench + rocprof summary, the full GPU suite, then PMC passes of the rolling kernels.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+TAG=${1:-r3e}
+timeout -k 10 400 python -u -m pytest tests/test_wgrad_roll_gpu.py tests/test_roll_gpu.py tests/test_multitile_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/$TAG.roll.log 2>&1
+rc=$?; echo "roll tests rc=$rc"; tail -15 gpurun_out/$TAG.roll.log; [ $rc -eq 0 ] || exit $rc
+for C in duf64 duf224v; do
+  timeout -k 10 200 python tools/conv_microbench.py --case $C --what fwdpro,dgrad,wgradpro >> gpurun_out/$TAG.micro.txt 2>&1 || exit $?
+done
+timeout -k 10 200 python tools/conv_microbench.py --case duf64 --what wgradpro --paths wgrad_roll=0 >> gpurun_out/$TAG.micro.txt 2>&1 || exit $?
+for P in "" "roll=0"; do
+  echo "-- edsr paths=$P" >> gpurun_out/$TAG.micro.txt
+  timeout -k 10 200 python tools/conv_microbench.py --case edsr3x3 --what fwd,relu,res,dgrad,mask,resacc --paths "$P" >> gpurun_out/$TAG.micro.txt 2>&1 || exit $?
+done
+cat gpurun_out/$TAG.micro.txt
+timeout -k 10 300 python bench.py --models edsr,duf --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/$TAG.bench.json 2> gpurun_out/$TAG.bench.err || exit $?
+python -c "
+import json
+for l in open('gpurun_out/$TAG.bench.json'):
+    if l.startswith('{'):
+        d = json.loads(l)
+        print({k: (v.get('ms_per_step'), v.get('roofline', {}).get('frac')) for k, v in d.get('models', {}).items()})
+"
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/$TAG.prof -o run -- python $GRAFT_REPO_ROOT/bench.py --models edsr,duf --steps 3 --warmup 1 --no-cpu-baseline --no-peaks > $GRAFT_REPO_ROOT/gpurun_out/$TAG.prof.log 2>&1)
+echo "prof rc=$?"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/$TAG.tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -15 gpurun_out/$TAG.tests.log; [ $rc -eq 0 ] || exit $rc
+i=0
+for CNT in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS" \
+           "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VMEM" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $CNT -d gpurun_out/$TAG.p$i -o run --output-format csv -- python tools/conv_microbench.py --case duf64 --iters 3 --what fwdpro,wgradpro > gpurun_out/$TAG.p$i.log 2>&1
+  echo "pass $i rc=$?"
+  timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $CNT -d gpurun_out/$TAG.e$i -o run --output-format csv -- python tools/conv_microbench.py --case edsr3x3 --iters 3 --what fwd > gpurun_out/$TAG.e$i.log 2>&1
+  echo "edsr pass $i rc=$?"
+done
+python tools/pmc_summary.py $(find gpurun_out/$TAG.p* -name "*counter_collection.csv") > gpurun_out/$TAG.pmc.txt
+python tools/pmc_summary.py $(find gpurun_out/$TAG.e* -name "*counter_collection.csv") > gpurun_out/$TAG.pmc_edsr.txt
+grep -A 30 "roll" gpurun_out/$TAG.pmc.txt | head -80

@@ -253,6 +253,17 @@ static inline bool chunk_ok(const vsrk_tensor5* t, int esize) {
 
 // pipelined 16-bit 3x3(x3) weight gradient (conv_wgrad_pipe.hip): 1 = launched the slab kernel, 0 = not eligible.
 int vsrk_conv_wgrad_pipe(const vsrk_conv::WgradArgs& a, int nco, int nci, int dtype, hipStream_t s);
+// rolling-depth 16-bit Conv3d 3x3x3 weight gradient (conv_wgrad_roll.hip):
+// plan (false = not eligible) and launch (1 = launched the slab kernel, whose
+// slabs wgrad_reduce_kernel sums over 2 * nsplit splits and 3 * nci * nco
+// combos; 0 = not eligible)
+bool vsrk_wgrad_roll_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk_tensor5* dy, int* nsplit,
+                          int* tps, int* ntiles, int* dzc, size_t* ws_bytes);
+int vsrk_conv_wgrad_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk_tensor5* dy,
+                         const float* pro_scale, const float* pro_shift, int want_bias, float* ws, size_t ws_bytes,
+                         int* nsplit_out, hipStream_t s);
+void vsrk_conv_set_wgrad_roll_mode(int mode);
+extern int vsrk_g_roll_dz;  // vsrk_conv_set_roll_depth (conv_roll.hip)
 // thin-channel weight gradient (conv_thin.hip): 1 = launched the slab kernel, 0 = not eligible.
 int vsrk_conv_wgrad_thin(const vsrk_conv::WgradArgs& a, int nco, int nci, int perm_r, int dtype, hipStream_t s);
 

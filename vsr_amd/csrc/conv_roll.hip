@@ -44,11 +44,31 @@ constexpr int RHW = TW + 2;                // 34 halo columns
 constexpr int RHROWS = (RFTH + 2) * RHW;   // 612 halo voxels
 constexpr int RCH = 16;                    // input channels per stage
 constexpr int RNAI = (RHROWS + 31) / 32;   // 20 A pieces (32 voxels x 32 B each)
-constexpr int RNBI = 27;                   // 27 B pieces (one tap: 32 channels x 32 B)
-constexpr int RNI = RNAI + RNBI;           // 47
-constexpr int RNQ = (RNI + RNW - 1) / RNW;  // 6 pieces per wave and stage
-constexpr int RSLOT = RNQ * RNW * 1024;    // 48 KB: A | B | one junk piece
+constexpr int RNA = (RNAI + RNW - 1) / RNW;  // 3: A pieces per wave (q < 3)
 constexpr int RNSLOT = 3;
+
+// Geometry of the two forms.  KD = 3, NT = 1: Conv3d 3x3x3, one 32-channel
+// output block, three accumulator banks (output depths).  KD = 1, NT = 2:
+// Conv 3x3 over depth-1 slices (a Conv2d on a D = 1 view), two 32-channel
+// output blocks sharing every A fragment (the 64-channel EDSR body convs).
+// B piece p = tap * NT + nt holds (tap, output block nt): 32 channels x 32 B.
+template <int KD, int NT>
+struct RollGeo {
+  static_assert((KD == 3 && NT == 1) || (KD == 1 && NT == 2), "rolling conv forms: 3x3x3 / 32 or 3x3 / 64");
+  static constexpr int NB = 9 * KD * NT;           // B pieces: 27 / 18
+  static constexpr int NI = RNAI + NB;             // 47 / 38
+  static constexpr int NQ = (NI + RNW - 1) / RNW;  // pieces per wave and stage: 6 / 5
+  static constexpr int SLOT = NQ * RNW * 1024;     // 48 KB / 40 KB: A | B | junk pieces
+  static constexpr int NACC = KD * NT;             // accumulator sets: banks (KD 3) or blocks (KD 1)
+  static constexpr int NG = 3 * NACC;              // compute groups (kw, set): 9 / 6
+  static constexpr int NTG = NG - NQ;              // groups that carry the late prologue: 3 / 1
+  static constexpr int TPG = (RNA + NTG - 1) / NTG;
+  static_assert(NTG >= 1, "a group must be left for the late prologue");
+};
+
+// Epilogue forms (compile time): out = fma(acc, out_scale, bias*out_scale)
+// [relu] [* (mask > 0)] [+ residual] [+ out]
+enum { RE_RES = 1, RE_MASK = 2, RE_ACC = 4, RE_RELU = 8 };
 
 // Division by a launch constant d (dividends < 2^31): q = (x * mul) >> p with
 // p = 31 + ceil(log2 d), mul = ceil(2^p / d).
@@ -71,7 +91,7 @@ struct RView {
 };
 
 struct RollArgs {
-  RView x, y;
+  RView x, y, res, msk;
   const void* w;
   const float* bias;
   const float* pro_scale;
@@ -92,8 +112,13 @@ __device__ __forceinline__ void roll_wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int PRO, int RELU, typename H>
+template <int KD, int NT, int PRO, int EM, typename H>
 __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
+  using G = RollGeo<KD, NT>;
+  constexpr int RNQ = G::NQ, RSLOT = G::SLOT, NACC = G::NACC;
+  // the residual / mask operand of a 2-D tile is loaded into registers during
+  // its last stage (one extra operand, no accumulate)
+  constexpr bool PREF = KD == 1 && ((EM & RE_RES) != 0) != ((EM & RE_MASK) != 0) && !(EM & RE_ACC);
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -107,9 +132,10 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // piece j = wave + RNW*q fills slot bytes [j KB, j+1 KB); lane l writes 16
   // bytes at j KB + 16 l.  A (j < RNAI): halo voxel v = 32 j + l/2 (row
   // hh = v / 34, column ww = v % 34), position l & 1 holds the logical piece
-  // p = (l & 1) ^ bit 3 of ww (8 channels).  B (j < RNI): tap j - RNAI,
-  // output channel l/2, piece p = (l & 1) ^ bit 3 of the channel.
-  // qa: the wave's A pieces (bit q); qkd[kd]: its B pieces of taps of depth kd.
+  // p = (l & 1) ^ bit 3 of ww (8 channels).  B (j < NI): piece j - RNAI =
+  // (tap, output block), output channel l/2, piece p = (l & 1) ^ bit 3 of
+  // the channel.  qa: the wave's A pieces (bit q); qkd[kd]: its B pieces of
+  // taps of depth kd.
   int rel[RNQ], hwv[RNQ];
   unsigned qa = 0, qkd0 = 0, qkd1 = 0, qkd2 = 0;
 #pragma unroll
@@ -124,18 +150,19 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       rel[q] = hh * a.x.sh + ww * a.x.sw + 8 * p;
       hwv[q] = v < RHROWS ? ((hh << 8) | ww) : -1;
       qa |= 1u << q;
-    } else if (j < RNI) {
+    } else if (j < G::NI) {
       const int co = lane >> 1;
       const int p = (lane & 1) ^ ((co >> 3) & 1);
-      rel[q] = ((j - RNAI) * a.cout_pad + co) * a.cin_pad + 8 * p;
-      const int kd = (j - RNAI) / 9;
+      const int tap = (j - RNAI) / NT, nt = (j - RNAI) % NT;
+      rel[q] = (tap * a.cout_pad + nt * 32 + co) * a.cin_pad + 8 * p;
+      const int kd = tap / 9;
       if (kd == 0) qkd0 |= 1u << q;
       else if (kd == 1) qkd1 |= 1u << q;
       else qkd2 |= 1u << q;
     }
   }
   // ds_read bases (bytes within a slot): A fragment (kw, halo row hr) at
-  // abase[kw] + hr * 34 * 32; B fragment (tap) at RNAI KB + tap KB + bbase.
+  // abase[kw] + hr * 34 * 32; B fragment (tap, block) at RNAI KB + piece KB + bbase.
   uint32_t abase[3];
 #pragma unroll
   for (int kw = 0; kw < 3; ++kw)
@@ -143,33 +170,34 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   const uint32_t bbase = (uint32_t)(RNAI * 1024 + r * 32 + 16 * (hf ^ ((r >> 3) & 1)));
 
   // ---- tiles of this workgroup (XCD group x owns a contiguous range) ----
-  const int G = gridDim.x;
+  const int G_ = gridDim.x;
   const int xg = blockIdx.x & 7, jb = blockIdx.x >> 3;
-  const int gx = (G >> 3) + (xg < (G & 7) ? 1 : 0);
-  const int cx = xg * (G >> 3) + min(xg, G & 7);
-  const int t_lo = (int)((int64_t)a.ntiles * cx / G);
-  const int t_hi = (int)((int64_t)a.ntiles * (cx + gx) / G);
+  const int gx = (G_ >> 3) + (xg < (G_ & 7) ? 1 : 0);
+  const int cx = xg * (G_ >> 3) + min(xg, G_ & 7);
+  const int t_lo = (int)((int64_t)a.ntiles * cx / G_);
+  const int t_hi = (int)((int64_t)a.ntiles * (cx + gx) / G_);
 
   // A tile as the walks need it.  Order: output-channel tile fastest (they
   // share the input), then the depth run, columns, rows, sample.
   struct RTile {
-    int h0, w0, n0, z0, z1, di_lo, nsl;
+    int h0, w0, n0, z0, z1, di_lo, nsl, nb;
     int xo;  // element offset of halo origin (nb, di = 0, h0 - ph, w0 - pw) in x
     int yo;  // element offset of (nb, dz = 0, h0, w0, n0) in y
   };
   auto decode = [&](int t) __attribute__((always_inline)) {
     RTile tl;
     int u = rdiv(t, a.ntn);
-    tl.n0 = (t - u * (int)a.ntn.d) * 32;
+    tl.n0 = (t - u * (int)a.ntn.d) * 32 * NT;
     int v = rdiv(u, a.nzc);
     tl.z0 = (u - v * (int)a.nzc.d) * a.dzc;
     u = rdiv(v, a.tiles_w);
     tl.w0 = (v - u * (int)a.tiles_w.d) * TW;
     const int nb = rdiv(u, a.tiles_h);
+    tl.nb = nb;
     tl.h0 = (u - nb * (int)a.tiles_h.d) * RFTH;
     tl.z1 = min(tl.z0 + a.dzc, a.y.d);
     tl.di_lo = max(0, tl.z0 - a.pd);
-    tl.nsl = min(a.x.d - 1, tl.z1 + 1 - a.pd) - tl.di_lo + 1;
+    tl.nsl = min(a.x.d - 1, tl.z1 + KD - 2 - a.pd) - tl.di_lo + 1;
     tl.xo = nb * a.x.sn + (tl.h0 - a.ph) * a.x.sh + (tl.w0 - a.pw) * a.x.sw;
     tl.yo = nb * a.y.sn + tl.h0 * a.y.sh + tl.w0 * a.y.sw + tl.n0;
     return tl;
@@ -189,8 +217,9 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // kd taps with an output depth inside [z0, z1) for input slice di
   auto kd_mask = [&](int z0, int z1, int di) __attribute__((always_inline)) {
     const int P = di + a.pd;
-    return (P >= z0 && P < z1 ? 1u : 0u) | (P - 1 >= z0 && P - 1 < z1 ? 2u : 0u) |
-           (P - 2 >= z0 && P - 2 < z1 ? 4u : 0u);
+    unsigned m = P >= z0 && P < z1 ? 1u : 0u;
+    if constexpr (KD == 3) m |= (P - 1 >= z0 && P - 1 < z1 ? 2u : 0u) | (P - 2 >= z0 && P - 2 < z1 ? 4u : 0u);
+    return m;
   };
 
   // ---- the DMA walk (two stages ahead of the compute walk) ----
@@ -218,7 +247,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   };
   // stage of walk k: A pieces of slice di, channels [c0, c0 + 16) (zero page
   // outside the image), B pieces of the weight slab (zero page for taps of a
-  // kd with no output depth in the tile), and the junk piece (zero page)
+  // kd with no output depth in the tile), and the junk pieces (zero page)
   auto prep = [&](const Walk& k) __attribute__((always_inline)) {
     Dma d;
     const int di = k.tl.di_lo + k.sl;
@@ -236,9 +265,9 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     glds16(src, lds_addr(lds) + slot * RSLOT + j * 1024);
   };
 
-  f32x16 acc[3][RMS];  // bank b: the output depth dz with dz % 3 == b
+  f32x16 acc[NACC][RMS];  // KD 3: bank b holds the output depth dz with dz % 3 == b; KD 1: output block b
 #pragma unroll
-  for (int k = 0; k < 3; ++k)
+  for (int k = 0; k < NACC; ++k)
 #pragma unroll
     for (int m = 0; m < RMS; ++m)
 #pragma unroll
@@ -257,25 +286,73 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     }
   };
 
-  // One stage on slot SLOT.  Groups (kw, bank b) in kw-major order: the 4
+  // Epilogue operand prefetch (2-D, one operand): 4 channels (8 bytes) per
+  // (row, block, channel group), the layout of the accumulator lanes.  The
+  // loads are inline asm like the DMA pieces: the compiler's own vmcnt
+  // bookkeeping cannot see those, and would drain the in-flight stage at the
+  // first use.  They are issued before the stage's DMA pieces, so the
+  // stage wait of the next step retires them; `settle` then ties the uses
+  // after that step's barrier.
+  typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+  u32x2_t pre[PREF ? RMS : 1][PREF ? NT : 1][4];
+  const RView& pv = (EM & RE_RES) ? a.res : a.msk;
+  auto prefetch = [&](const RTile& tl, int dz) __attribute__((always_inline)) {
+    if constexpr (PREF) {
+#pragma unroll
+      for (int ms = 0; ms < RMS; ++ms) {
+        const int ho = tl.h0 + wave * RMS + ms, wo = tl.w0 + r;
+        const bool ok = ho < a.y.h && wo < a.y.w;
+        const H* pp = reinterpret_cast<const H*>(pv.ptr) +
+                      (tl.nb * pv.sn + dz * pv.sd + ho * pv.sh + wo * pv.sw + tl.n0 + 4 * hf);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const bool okc = ok && tl.n0 + nt * 32 + 8 * g + 4 * hf < a.cout;
+            const void* src = okc ? (const void*)(pp + nt * 32 + 8 * g) : (const void*)zp;
+            asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(pre[ms][nt][g]) : "v"(src) : "memory");
+          }
+      }
+    }
+  };
+  auto settle = [&]() __attribute__((always_inline)) {
+    if constexpr (PREF) {
+#pragma unroll
+      for (int ms = 0; ms < RMS; ++ms)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) asm volatile("" : "+v"(pre[ms][nt][g]));
+    }
+  };
+
+  // One stage on slot SLOT.  Groups (kw, set b) in kw-major order: the 4
   // A fragments (halo rows) of a kw are read one kw ahead, the 3 B fragments
-  // of a group (taps (kd_b, kh, kw); kd_b = the tap whose output depth lives
-  // in bank b) one group ahead, both unconditionally (an idle kd's taps are
-  // zeros), then 6 MFMAs if bank b has work.  Groups 0-5 each issue one DMA
-  // piece of the stage two ahead (slot SLOT+2); groups 6-8 apply the BN/ReLU
-  // prologue to this wave's A pieces of the NEXT stage (slot SLOT+1, landed
-  // one stage ago), beside the MFMAs instead of in front of the barrier.
+  // of a group (taps (kd_b, kh, kw) of set b: KD 3, the tap whose output
+  // depth lives in bank b; KD 1, output block b) one group ahead, both
+  // unconditionally (an idle kd's taps are zeros), then 3 x RMS MFMAs if set
+  // b has work.  Groups 0..NQ-1 each issue one DMA piece of the stage two
+  // ahead (slot SLOT+2); the remaining groups apply the BN/ReLU prologue to
+  // this wave's A pieces of the NEXT stage (slot SLOT+1, landed one stage
+  // ago), beside the MFMAs instead of in front of the barrier.
   auto compute = [&](auto slot_c, int P, unsigned km, const Dma& dn, bool don, bool tnext, int tc,
                      unsigned tm) __attribute__((always_inline)) {
     constexpr int SLOT = decltype(slot_c)::value;
     const char* sl = lds + SLOT * RSLOT;
     char* sl1 = lds + ((SLOT + 1) % 3) * RSLOT;
     const int pm = P % 3;
-    uint32_t bofs[3];  // byte offset of the taps of the kd whose output depth is in bank b
+    uint32_t bofs[NACC];  // byte offset of set b's taps
+    unsigned bm;          // sets with work
+    if constexpr (KD == 3) {
 #pragma unroll
-    for (int b = 0; b < 3; ++b) bofs[b] = (uint32_t)(((pm + 3 - b) % 3) * 9 * 1024);
-    const unsigned bm = ((km & 1) ? (1u << pm) : 0u) | ((km & 2) ? (1u << ((pm + 2) % 3)) : 0u) |
-                        ((km & 4) ? (1u << ((pm + 1) % 3)) : 0u);  // banks with work
+      for (int b = 0; b < 3; ++b) bofs[b] = (uint32_t)(((pm + 3 - b) % 3) * 9 * 1024);
+      bm = ((km & 1) ? (1u << pm) : 0u) | ((km & 2) ? (1u << ((pm + 2) % 3)) : 0u) |
+           ((km & 4) ? (1u << ((pm + 1) % 3)) : 0u);
+    } else {
+#pragma unroll
+      for (int b = 0; b < NACC; ++b) bofs[b] = (uint32_t)(b * 1024);
+      bm = (km & 1) ? (1u << NACC) - 1 : 0u;
+    }
     uint4 ax[2][RMS + 2];
     uint4 bw[2][3];
     auto load_a = [&](uint4* af, int kw) __attribute__((always_inline)) {
@@ -283,25 +360,28 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       for (int hr = 0; hr < RMS + 2; ++hr) af[hr] = *reinterpret_cast<const uint4*>(sl + abase[kw] + hr * RHW * 32);
     };
     auto load_b = [&](uint4* bf, int g) __attribute__((always_inline)) {
-      const int kw = g / 3, b = g % 3;
-      const char* pb = sl + bbase + bofs[b] + kw * 1024;
+      const int kw = g / NACC, b = g % NACC;
+      const char* pb = sl + bbase + bofs[b] + kw * NT * 1024;
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh) bf[kh] = *reinterpret_cast<const uint4*>(pb + kh * 3 * 1024);
+      for (int kh = 0; kh < 3; ++kh) bf[kh] = *reinterpret_cast<const uint4*>(pb + kh * 3 * NT * 1024);
     };
     load_a(ax[0], 0);
     load_b(bw[0], 0);
 #pragma unroll
-    for (int g = 0; g < 9; ++g) {
-      const int kw = g / 3, b = g % 3;
-      if (g + 1 < 9) load_b(bw[(g + 1) & 1], g + 1);
-      if (b == 1 && kw + 1 < 3) load_a(ax[(kw + 1) & 1], kw + 1);
+    for (int g = 0; g < G::NG; ++g) {
+      const int kw = g / NACC, b = g % NACC;
+      if (g + 1 < G::NG) load_b(bw[(g + 1) & 1], g + 1);
+      if (b == (NACC == 3 ? 1 : 0) && kw + 1 < 3) load_a(ax[(kw + 1) & 1], kw + 1);
       if (g < RNQ && don) dma(dn, g, (SLOT + 2) % 3);
       if constexpr (PRO) {
         if (g == RNQ && tnext) {
           if (don) roll_wait_vmcnt<RNQ>();  // the next stage's pieces landed (the one after stays in flight)
           else roll_wait_vmcnt<0>();
         }
-        if (g >= RNQ && tnext) transform_piece(sl1, g - RNQ, tc, tm);
+        if (g >= RNQ && tnext) {
+#pragma unroll
+          for (int q = (g - RNQ) * G::TPG; q < (g - RNQ + 1) * G::TPG && q < RNA; ++q) transform_piece(sl1, q, tc, tm);
+        }
       }
       if ((bm >> b) & 1) {
 #pragma unroll
@@ -312,25 +392,59 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     }
   };
 
-  // Epilogue of one finished output depth dz of a tile: out = [relu](acc *
-  // out_scale + bias * out_scale), 4 channels (8 bytes) per lane.
+  // Epilogue of one finished output depth dz of a tile, output block nt:
+  // 4 channels (8 bytes) per lane and channel group.
   const float osc = a.out_scale;
-  auto epilogue = [&](const f32x16 (&A)[RMS], const RTile& tl, int dz) __attribute__((always_inline)) {
+  auto epilogue = [&](const f32x16 (&A)[RMS], const RTile& tl, int dz, int nt, bool use_pre)
+                      __attribute__((always_inline)) {
 #pragma unroll
     for (int ms = 0; ms < RMS; ++ms) {
       const int ho = tl.h0 + wave * RMS + ms, wo = tl.w0 + r;
       if (ho < a.y.h && wo < a.y.w) {
-        H* yp = reinterpret_cast<H*>(a.y.ptr) + (tl.yo + dz * a.y.sd + (wave * RMS + ms) * a.y.sh + r * a.y.sw + 4 * hf);
+        H* yp = reinterpret_cast<H*>(a.y.ptr) +
+                (tl.yo + dz * a.y.sd + (wave * RMS + ms) * a.y.sh + r * a.y.sw + nt * 32 + 4 * hf);
+        const H* rp = nullptr;
+        const H* mp = nullptr;
+        if constexpr (EM & RE_RES)
+          rp = reinterpret_cast<const H*>(a.res.ptr) +
+               (tl.nb * a.res.sn + dz * a.res.sd + ho * a.res.sh + wo * a.res.sw + tl.n0 + nt * 32 + 4 * hf);
+        if constexpr (EM & RE_MASK)
+          mp = reinterpret_cast<const H*>(a.msk.ptr) +
+               (tl.nb * a.msk.sn + dz * a.msk.sd + ho * a.msk.sh + wo * a.msk.sw + tl.n0 + nt * 32 + 4 * hf);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int co = tl.n0 + 8 * g + 4 * hf;
+          const int co = tl.n0 + nt * 32 + 8 * g + 4 * hf;
           if (co < a.cout) {
             const float4 bs = *reinterpret_cast<const float4*>(lbias + co);
             float v[4] = {fmaf(A[ms][4 * g + 0], osc, bs.x), fmaf(A[ms][4 * g + 1], osc, bs.y),
                           fmaf(A[ms][4 * g + 2], osc, bs.z), fmaf(A[ms][4 * g + 3], osc, bs.w)};
-            if constexpr (RELU) {
+            if constexpr (EM & RE_RELU) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+            }
+            if constexpr (EM & RE_MASK) {
+              uint2 mv;
+              if constexpr (PREF) mv = use_pre ? __builtin_bit_cast(uint2, pre[ms][nt][g]) : *reinterpret_cast<const uint2*>(mp + 8 * g);
+              else mv = *reinterpret_cast<const uint2*>(mp + 8 * g);
+              float mm[4];
+              unpack_pk<H>(mv, mm);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = mm[e] > 0.f ? v[e] : 0.f;
+            }
+            if constexpr (EM & RE_RES) {
+              uint2 rv;
+              if constexpr (PREF) rv = use_pre ? __builtin_bit_cast(uint2, pre[ms][nt][g]) : *reinterpret_cast<const uint2*>(rp + 8 * g);
+              else rv = *reinterpret_cast<const uint2*>(rp + 8 * g);
+              float rr[4];
+              unpack_pk<H>(rv, rr);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += rr[e];
+            }
+            if constexpr (EM & RE_ACC) {
+              float o[4];
+              unpack_pk<H>(*reinterpret_cast<const uint2*>(yp + 8 * g), o);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += o[e];
             }
             *reinterpret_cast<uint2*>(yp + 8 * g) = pack_pk<H, uint2>(v);
           }
@@ -338,18 +452,30 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       }
     }
   };
-  // Flush after slice pdi of tile tl: the banks whose output depth takes no
-  // more contributions -- dz = pdi + pd - 2 when the walk stays in the tile
-  // (all = false), every bank at the end of the tile -- are stored (if inside
-  // the tile's depth run) and zeroed.
-  auto flush = [&](const RTile& tl, int pdi, bool all) __attribute__((always_inline)) {
+  // Flush after slice pdi of tile tl.  KD 3: the banks whose output depth
+  // takes no more contributions -- dz = pdi + pd - 2 when the walk stays in
+  // the tile (all = false), every bank at the end of the tile -- are stored
+  // (if inside the tile's depth run) and zeroed.  KD 1: output depth pdi + pd,
+  // every block.
+  auto flush = [&](const RTile& tl, int pdi, bool all, bool use_pre) __attribute__((always_inline)) {
     const int P = pdi + a.pd;
-    const int bdone = (P + 1) % 3;  // bank of P - 2
+    if constexpr (KD == 3) {
+      const int bdone = (P + 1) % 3;  // bank of P - 2
 #pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      if (all || b == bdone) {
-        const int dz = P - (P + 3 - b) % 3;  // the output depth in bank b
-        if (dz >= tl.z0 && dz < tl.z1) epilogue(acc[b], tl, dz);
+      for (int b = 0; b < 3; ++b) {
+        if (all || b == bdone) {
+          const int dz = P - (P + 3 - b) % 3;  // the output depth in bank b
+          if (dz >= tl.z0 && dz < tl.z1) epilogue(acc[b], tl, dz, 0, false);
+#pragma unroll
+          for (int m = 0; m < RMS; ++m)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[b][m][i] = 0.f;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < NACC; ++b) {
+        if (P >= tl.z0 && P < tl.z1) epilogue(acc[b], tl, P, b, use_pre);
 #pragma unroll
         for (int m = 0; m < RMS; ++m)
 #pragma unroll
@@ -397,18 +523,31 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     if (tnext) roll_wait_vmcnt<RNQ>();
     else roll_wait_vmcnt<0>();
 #pragma unroll
-    for (int q = 0; q < RNQ; ++q) transform_piece(lds, q, 0, cm);
+    for (int q = 0; q < RNA; ++q) transform_piece(lds, q, 0, cm);
   }
   RTile ptl = ct;
   int pdi = -1;     // slice whose end is still to be flushed (-1: none)
   bool pall = false;
+  bool ppre = false;  // its epilogue operand was prefetched
   // one stage; false when it was the workgroup's last
   auto step = [&](auto slot_c) __attribute__((always_inline)) -> bool {
-    if (tnext) roll_wait_vmcnt<RNQ>();  // this stage landed; the next stays in flight
+    if (tnext) roll_wait_vmcnt<RNQ>();  // this stage landed (and any prefetch); the next stays in flight
     else roll_wait_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // this slot ready, the previous one free
-    if (pdi >= 0) flush(ptl, pdi, pall);
+    if (pdi >= 0) {
+      if (ppre) settle();
+      flush(ptl, pdi, pall, ppre);
+    }
     const int di = ct.di_lo + cs;
+    // the tile's last chunk of a slice that completes a 2-D output depth:
+    // its epilogue operand is loaded now, before this stage's DMA pieces
+    ppre = false;
+    if constexpr (PREF) {
+      if (cc == a.nchunk - 1 && di + a.pd >= ct.z0 && di + a.pd < ct.z1) {
+        prefetch(ct, di + a.pd);
+        ppre = true;
+      }
+    }
     Dma dn;
     dn.xb = nullptr;
     dn.wsrc = nullptr;
@@ -439,11 +578,12 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   while (step(std::integral_constant<int, 0>{}) && step(std::integral_constant<int, 1>{}) &&
          step(std::integral_constant<int, 2>{})) {
   }
-  flush(ptl, pdi, true);
+  roll_wait_vmcnt<0>();  // the last stage's prefetch
+  if (ppre) settle();
+  flush(ptl, pdi, true, ppre);
 }
 
 int g_roll_mode = -1;  // -1: from VSRK_CONV_ROLL (default on), 0 off, 1 on
-int g_roll_dz = 0;     // > 0: output depths per tile (test knob), 0: automatic
 
 int roll_num_cus() {
   static int n = 0;
@@ -455,9 +595,9 @@ int roll_num_cus() {
   return n;
 }
 
-template <int PRO, int RELU, typename H>
+template <int KD, int NT, int PRO, int EM, typename H>
 int launch_roll(const RollArgs& a, size_t lds, int grid, hipStream_t s) {
-  auto kern = conv_roll_kernel<PRO, RELU, H>;
+  auto kern = conv_roll_kernel<KD, NT, PRO, EM, H>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   kern<<<grid, RNW * 64, lds, s>>>(a);
   VSRK_LAUNCH_CHECK("conv_fwd(roll)");
@@ -466,9 +606,12 @@ int launch_roll(const RollArgs& a, size_t lds, int grid, hipStream_t s) {
 
 }  // namespace
 
+// > 0: output depths per tile of both rolling kernels (test knob), 0: automatic
+int vsrk_g_roll_dz = 0;
+
 extern "C" int vsrk_conv_set_roll_depth(int32_t depths) {
   VSRK_CHECK(depths >= 0, "conv_set_roll_depth: depths must be >= 0");
-  g_roll_dz = depths;
+  vsrk_g_roll_dz = depths;
   return VSRK_OK;
 }
 
@@ -484,14 +627,26 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   }
   if (g_roll_mode == 0) return 0;
   if (!vsrk_is16(x->dtype) || y->dtype != x->dtype) return 0;
-  if (d->kd != 3 || d->kh != 3 || d->kw != 3) return 0;
-  if (residual || mask || d->accumulate || d->bias_perm_r > 1 || d->act == VSRK_ACT_PRELU) return 0;
+  if (d->kh != 3 || d->kw != 3) return 0;
+  // the two forms: Conv3d 3x3x3 (32-channel output blocks) and 3x3 over
+  // depth-1 slices with 64-channel output blocks (cout a multiple of 64)
+  const bool k3 = d->kd == 3;
+  if (!k3 && !(d->kd == 1 && d->pd == 0 && y->c % 64 == 0)) return 0;
+  if (d->bias_perm_r > 1 || d->act == VSRK_ACT_PRELU || d->mask_slope) return 0;
+  if (k3 && (residual || mask || d->accumulate)) return 0;
   if (x->shuffle > 1 || y->shuffle > 1) return 0;
   if (x->c % RCH != 0 || !chunk_ok(x, 2)) return 0;
   if (d->pd < 0 || d->pd > 2 || d->ph < 0 || d->ph > 2 || d->pw < 0 || d->pw > 2) return 0;
-  if (y->d != x->d + 2 * d->pd - 2 || y->h != x->h + 2 * d->ph - 2 || y->w != x->w + 2 * d->pw - 2) return 0;
-  if (y->c % 4 != 0 || ((uintptr_t)y->ptr) % 8 != 0 || y->sn % 4 || y->sd % 4 || y->sh % 4 || y->sw % 4) return 0;
-  for (const vsrk_tensor5* t : {x, y}) {  // every element offset fits in 32 bits
+  if (y->d != x->d + 2 * d->pd - (d->kd - 1) || y->h != x->h + 2 * d->ph - 2 || y->w != x->w + 2 * d->pw - 2) return 0;
+  auto out_ok = [&](const vsrk_tensor5* t) {  // 8-byte epilogue accesses, the output's geometry
+    return t->dtype == y->dtype && t->shuffle <= 1 && t->n == y->n && t->d == y->d && t->h == y->h && t->w == y->w &&
+           t->c == y->c && ((uintptr_t)t->ptr) % 8 == 0 && t->sn % 4 == 0 && t->sd % 4 == 0 && t->sh % 4 == 0 &&
+           t->sw % 4 == 0;
+  };
+  if (y->c % 4 != 0 || !out_ok(y)) return 0;
+  if ((residual && !out_ok(residual)) || (mask && !out_ok(mask))) return 0;
+  for (const vsrk_tensor5* t : {x, y, residual, mask}) {  // every element offset fits in 32 bits
+    if (!t) continue;
     const int64_t span = (int64_t)(t->n - 1) * t->sn + (int64_t)(t->d - 1) * t->sd + (int64_t)(t->h - 1) * t->sh +
                          (int64_t)(t->w - 1) * t->sw + t->c + 2 * (int64_t)RHW * t->sw + (RFTH + 2) * t->sh;
     if (span >= (1ll << 31) || t->sn < 0 || t->sd < 0 || t->sh < 0 || t->sw < 0) return 0;
@@ -506,6 +661,8 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   RollArgs a;
   a.x = rview(x);
   a.y = rview(y);
+  a.res = rview(residual ? residual : y);
+  a.msk = rview(mask ? mask : y);
   a.w = w_packed;
   a.bias = bias;
   a.pro_scale = pro_scale;
@@ -520,20 +677,23 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   a.prologue = d->prologue;
   a.out_scale = d->out_scale;
   a.nchunk = x->c / RCH;
-  const int tiles_h = ceil_div(y->h, RFTH), tiles_w = ceil_div(y->w, TW), ntn = ceil_div(y->c, 32);
+  const int nt = k3 ? 1 : 2;
+  const int tiles_h = ceil_div(y->h, RFTH), tiles_w = ceil_div(y->w, TW), ntn = ceil_div(y->c, 32 * nt);
   const int64_t spatial = (int64_t)y->n * tiles_h * tiles_w * ntn;
   if (spatial == 0 || y->d == 0) return 1;
   // Depth run per tile: as long as possible (each input slice then serves
   // three output depths) while the grid still gets >= 2 tiles per CU.
   int dzc = y->d;
-  if (g_roll_dz > 0) {
-    dzc = std::min(g_roll_dz, y->d);
-  } else {
+  if (vsrk_g_roll_dz > 0) {
+    dzc = std::min(vsrk_g_roll_dz, y->d);
+  } else if (k3) {
     const int64_t want = 2 * (int64_t)roll_num_cus();
     if (spatial < want) {
       const int64_t runs = std::min<int64_t>(ceil_div64(want, spatial), y->d);
       dzc = (int)ceil_div64(y->d, runs);
     }
+  } else {
+    dzc = 1;  // 2-D: a tile is one slice
   }
   a.dzc = dzc;
   const int nzc = ceil_div(y->d, dzc);
@@ -544,14 +704,31 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   const int64_t ntiles = spatial * nzc;
   VSRK_CHECK(ntiles < (1ll << 31), "conv_fwd(roll): too many tiles");
   a.ntiles = (int)ntiles;
-  const size_t lds = (size_t)RNSLOT * RSLOT + (size_t)a.cout_pad * 4 + (d->prologue ? 2 * (size_t)a.cin_pad * 4 : 0);
+  const size_t slot = k3 ? RollGeo<3, 1>::SLOT : RollGeo<1, 2>::SLOT;
+  const size_t lds = (size_t)RNSLOT * slot + (size_t)a.cout_pad * 4 + (d->prologue ? 2 * (size_t)a.cin_pad * 4 : 0);
   if (lds > 160 * 1024) return 0;
   const int grid = (int)vsrk_capped_grid(std::min<int64_t>(ntiles, roll_num_cus()));
   const bool relu = d->act == VSRK_ACT_RELU;
+  const int em = (residual ? RE_RES : 0) | (mask ? RE_MASK : 0) | (d->accumulate ? RE_ACC : 0) | (relu ? RE_RELU : 0);
   int rc = vsrk_dispatch16(x->dtype, [&](auto tag) {
     using H = decltype(tag);
-    if (d->prologue) return relu ? launch_roll<1, 1, H>(a, lds, grid, s) : launch_roll<1, 0, H>(a, lds, grid, s);
-    return relu ? launch_roll<0, 1, H>(a, lds, grid, s) : launch_roll<0, 0, H>(a, lds, grid, s);
+    if (k3) {
+      if (d->prologue) return relu ? launch_roll<3, 1, 1, RE_RELU, H>(a, lds, grid, s) : launch_roll<3, 1, 1, 0, H>(a, lds, grid, s);
+      return relu ? launch_roll<3, 1, 0, RE_RELU, H>(a, lds, grid, s) : launch_roll<3, 1, 0, 0, H>(a, lds, grid, s);
+    }
+    // 2-D forms of the EDSR body and its backward: plain, ReLU, residual,
+    // ReLU mask, residual + accumulate (with or without the BN prologue: none
+    // of EDSR's convs has one, the generic path serves it)
+    if (d->prologue) return (int)VSRK_ERR_UNSUPPORTED;
+    switch (em) {
+      case 0: return launch_roll<1, 2, 0, 0, H>(a, lds, grid, s);
+      case RE_RELU: return launch_roll<1, 2, 0, RE_RELU, H>(a, lds, grid, s);
+      case RE_RES: return launch_roll<1, 2, 0, RE_RES, H>(a, lds, grid, s);
+      case RE_MASK: return launch_roll<1, 2, 0, RE_MASK, H>(a, lds, grid, s);
+      case RE_RES | RE_ACC: return launch_roll<1, 2, 0, RE_RES | RE_ACC, H>(a, lds, grid, s);
+      default: return (int)VSRK_ERR_UNSUPPORTED;
+    }
   });
+  if (rc == VSRK_ERR_UNSUPPORTED) return 0;
   return rc == VSRK_OK ? 1 : -rc;
 }

@@ -384,7 +384,10 @@ static WgradPlan wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, cons
 
 extern "C" size_t vsrk_conv_wgrad_workspace_size(const vsrk_conv_desc* d, const vsrk_tensor5* x,
                                                  const vsrk_tensor5* dy) {
-  return std::max(wgrad_plan(d, x, dy).ws_bytes, vsrk_conv_wgrad_pw_workspace(d, x, dy));
+  int ns, tps, nt, dzc;
+  size_t roll = 0;
+  if (!vsrk_wgrad_roll_plan(d, x, dy, &ns, &tps, &nt, &dzc, &roll)) roll = 0;
+  return std::max(std::max(wgrad_plan(d, x, dy).ws_bytes, vsrk_conv_wgrad_pw_workspace(d, x, dy)), roll);
 }
 
 template <typename T, int NCO, int NCI, int KK, bool VEC>
@@ -423,6 +426,21 @@ extern "C" int vsrk_conv_wgrad(const vsrk_conv_desc* d, const vsrk_tensor5* x, c
   const int pw = vsrk_conv_wgrad_pw(d, x, dy, pro_scale, pro_shift, dy_scale, perm_r, dw, dbias, accumulate,
                                     workspace, workspace_bytes, s);
   if (pw != 0) return pw > 0 ? VSRK_OK : -pw;
+  if (workspace && dy->n * dy->d * dy->h * dy->w > 0) {
+    // rolling-depth 3x3x3 kernel (conv_wgrad_roll.hip): its slabs, the same reduce
+    int ns = 0;
+    if (vsrk_conv_wgrad_roll(d, x, dy, pro_scale, pro_shift, dbias != nullptr, (float*)workspace, workspace_bytes,
+                             &ns, s)) {
+      VSRK_LAUNCH_CHECK("conv_wgrad(roll)");
+      const int nci = x->c / 32, nco = dy->c / 32;
+      const int64_t total = (int64_t)dy->c * x->c * 27 + (dbias ? dy->c : 0);
+      wgrad_reduce_kernel<<<(int)ceil_div64(total, 64), 256, 0, s>>>(
+          (const float*)workspace, dw, dbias, 2 * ns, 3 * nci * nco, 9 * 1024 + 32, dy->c, x->c, 3, 3, 3, nco, nci, 32,
+          32, std::min(d->pd, 2), perm_r, dy_scale, accumulate);
+      VSRK_LAUNCH_CHECK("conv_wgrad_reduce");
+      return VSRK_OK;
+    }
+  }
   const WgradPlan p = wgrad_plan(d, x, dy);
   VSRK_CHECK(workspace && workspace_bytes >= p.ws_bytes, "conv_wgrad: workspace %zu < %zu bytes", workspace_bytes,
              p.ws_bytes);

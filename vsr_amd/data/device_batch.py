@@ -23,6 +23,20 @@ from .datasets import _window
 from .transforms import Compose, Normalize, ToTensor, compose, plan_augments
 
 
+def _normalize(v: torch.Tensor, mean: float, std: float) -> torch.Tensor:
+    """(v - mean) / (std + 1e-10) with the reference's float32 rounding
+    (transforms.py:164-168 on float32 images: numpy casts both Python scalars
+    to float32, subtracts, then divides correctly rounded).  A device kernel
+    dividing by a Python scalar multiplies by its reciprocal instead (1 ulp
+    apart on some values), so the quotient is taken in float64 -- exact
+    division of two float32 values, then one rounding to float32, which is the
+    correctly rounded float32 quotient."""
+    dev = v.device
+    m = torch.tensor(mean, dtype=torch.float32, device=dev)
+    s = torch.tensor(std + 1e-10, dtype=torch.float32, device=dev).double()
+    return ((v.float() - m).double() / s).float()
+
+
 class DeviceCineBatcher:
     """Batches of (volume, target frame) items for one task.
 
@@ -45,9 +59,7 @@ class DeviceCineBatcher:
         if not lr.is_cuda or not hr.is_cuda:
             raise RuntimeError("DeviceCineBatcher keeps the volumes in device memory (no CPU fallback)")
         if normalize is not None:
-            mean, std = normalize
-            lr = (lr - mean) / (std + 1e-10)
-            hr = (hr - mean) / (std + 1e-10)
+            lr, hr = _normalize(lr, *normalize), _normalize(hr, *normalize)
         self.lr = lr.float().contiguous()
         self.hr = hr.float().contiguous()
         self.task = task

@@ -126,6 +126,12 @@ class SyncBNAllReduce:
     def __call__(self, t: torch.Tensor) -> None:
         dist.all_reduce(t, group=self.group)
 
+    def start(self, t: torch.Tensor):
+        """Asynchronous form: returns the work handle; ``handle.wait()`` makes the
+        current stream wait for the sum (no host block on RCCL), so independent
+        kernels queued in between (a weight gradient) hide the collective."""
+        return dist.all_reduce(t, group=self.group, async_op=True)
+
     def global_count(self, local: int) -> int:
         """Sum of `local` over the ranks (exact in float64 up to 2^53)."""
         dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(self.group) == "nccl" else "cpu"

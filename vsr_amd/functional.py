@@ -206,13 +206,13 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, k, pad, dw: torch.Tensor, dbia
 
 
 def set_conv_path(path: str, mode: int) -> None:
-    """Select a conv kernel family ("fast", "pw", "roll", "thin", "wgrad_pipe"): -1 default, 0 off, 1 on."""
+    """Select a conv kernel family ("fast", "pw", "roll", "thin", "wgrad_pipe", "wgrad_roll"): -1 default, 0 off, 1 on."""
     N.check(_lib().vsrk_conv_set_path(path.encode(), int(mode)), "conv_set_path")
 
 
 def set_roll_depth(depths: int) -> None:
     """Test knob: output depths per tile of the rolling-depth Conv3d 3x3x3
-    kernel (0 = automatic)."""
+    kernels, forward/dgrad and weight gradient (0 = automatic)."""
     N.check(_lib().vsrk_conv_set_roll_depth(int(depths)), "conv_set_roll_depth")
 
 

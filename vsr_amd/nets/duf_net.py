@@ -118,13 +118,12 @@ class DUFNet(BaseNet):
         st.count = count
         return st
 
-    def _bn_backward(self, bn, x, dz, st, dx, accumulate, grads):
-        red = self._bn_backward_reduce(bn, x, dz, st, grads)
-        F.bn_relu_bwd_apply(x, dz, st, bn.weight, red, st.count, dx, accumulate)
-
     def _bn_backward_reduce(self, bn, x, dz, st, grads):
         """The reduce half of the BN+ReLU backward: writes dgamma / dbeta and
-        returns the (sum_dy, sum_dy_xhat) that feed the input gradient."""
+        returns (the (sum_dy, sum_dy_xhat) that feed the input gradient, the
+        work handle of their SyncBN all-reduce or None).  The all-reduce is
+        asynchronous: the caller queues independent work (a weight gradient)
+        before waiting on the handle."""
         red = F.bn_relu_bwd_reduce(x, dz, st)
         # dgamma / dbeta are this rank's local sums: the data-parallel gradient
         # average (GradSync) combines them across ranks, as torch's
@@ -134,12 +133,13 @@ class DUFNet(BaseNet):
         gb = self._grad_buffer(bn.bias)
         gw.copy_(red[1])
         gb.copy_(red[0])
+        work = None
         if self.bn_allreduce is not None and st.count != float("inf"):
             red = red.clone()
-            self.bn_allreduce(red)
+            work = self.bn_allreduce.start(red)
         self._grad_done(grads, bn.weight, gw)
         self._grad_done(grads, bn.bias, gb)
-        return red
+        return red, work
 
     # ----------------------------------------------------------------------
     def _run(self, inputs, tape: dict | None):
@@ -268,10 +268,15 @@ class DUFNet(BaseNet):
         # right before the unit that needs it -- the head block at the end.
         # (lo, hi, f, dz, st, gamma, red, count) of the BNs done so far: the
         # tail's bn over every channel at the last depth, then each unit's bn1
-        red_t = self._bn_backward_reduce(dl.tail.bn, Rt, dzt, stt, grads)
+        red_t, work_t = self._bn_backward_reduce(dl.tail.bn, Rt, dzt, stt, grads)
         pending = [(lo, hi, ctot, dzt, stt, dl.tail.bn.weight, red_t, stt.count)]
+        works = [work_t]  # SyncBN all-reduces in flight (waited before their sums are used)
 
         def flush(dlo, dhi, c0, c1):
+            for wk in works:
+                if wk is not None:
+                    wk.wait()
+            works.clear()
             xs, out = C[:, dlo:dhi, :, :, c0:c1], dC[:, dlo:dhi, :, :, c0:c1]
             cs = [(dz[..., c0:c1], plo - dlo, st[:, c0:c1], gm[c0:c1] if gm is not None else None, red[:, c0:c1], cnt)
                   for plo, phi, pf, dz, st, gm, red, cnt in pending]
@@ -284,13 +289,19 @@ class DUFNet(BaseNet):
             R = C[:, lo:hi, :, :, :f]
             flush(olo, ohi, f, f + g)
             dx_i = dC[:, olo:ohi, :, :, f:f + g]
-            wgrad(u.conv2, t1, dx_i, (3, 3, 3), pad, prologue=ARF, pro_scale=st2[0], pro_shift=st2[1])
+            # each weight gradient is queued between a BatchNorm reduce and the
+            # use of its (SyncBN all-reduced) sums, so it hides the collective
             dz2 = dgrad(u.conv2, dx_i, torch.empty_like(t1), (3, 3, 3), pad)
+            red2, work2 = self._bn_backward_reduce(u.bn2, t1, dz2, st2, grads)
+            wgrad(u.conv2, t1, dx_i, (3, 3, 3), pad, prologue=ARF, pro_scale=st2[0], pro_shift=st2[1])
+            if work2 is not None:
+                work2.wait()
             dt1 = torch.empty_like(t1)
-            self._bn_backward(u.bn2, t1, dz2, st2, dt1, False, grads)
-            wgrad(u.conv1, R, dt1, K1, P0, prologue=ARF, pro_scale=st1[0], pro_shift=st1[1])
+            F.bn_relu_bwd_apply(t1, dz2, st2, u.bn2.weight, red2, st2.count, dt1, False)
             dz1 = dgrad(u.conv1, dt1, dz2, K1, P0)  # dz2 is dead: reuse its storage
-            red1 = self._bn_backward_reduce(u.bn1, R, dz1, st1, grads)
+            red1, work1 = self._bn_backward_reduce(u.bn1, R, dz1, st1, grads)
+            works.append(work1)
+            wgrad(u.conv1, R, dt1, K1, P0, prologue=ARF, pro_scale=st1[0], pro_shift=st1[1])
             pending.append((lo, hi, f, dz1, st1, u.bn1.weight, red1, st1.count))
         flush(0, C.shape[1], 0, 64)
         wgrad(self.head, tape["xv"], dC[..., :64], (1, 3, 3), (0, 1, 1))

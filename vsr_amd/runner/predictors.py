@@ -19,7 +19,10 @@ was removed from SciPy and imageio is not a dependency here); checkpoints
 load with ``weights_only=True`` (a reference checkpoint's pickled Monitor
 resolves through the same allow-list as the trainer's); the SISR / MISR
 predictors also write the GIF of the LAST sequence, which the reference's
-loop never flushes (acdc_sisr_predictor.py:72-79 only writes on a change).
+loop never flushes (acdc_sisr_predictor.py:72-79 only writes on a change),
+and start a new GIF when the patient changes even if the sequence id does
+not (the reference keys on the sequence id alone, so two consecutive
+single-slice patients would share one GIF).
 """
 from __future__ import annotations
 
@@ -153,7 +156,7 @@ class BasePredictor:
         frame; acdc_misr_predictor.py:66-91, acdc_sisr_predictor.py:66-90)."""
         row = torch.cat([metrics, losses], dim=1)[0].cpu().tolist()
         results.append([self._row_name(filename, fid), *row])
-        if sid != state["sid"]:
+        if (patient, sid) != (state["patient"], state["sid"]):
             self._flush_video(state)
         img = self._to_uint8(outs[0])
         state["sr_imgs"].append(img)
