@@ -13,7 +13,9 @@ and inputs, and compares the output, the PSNR of the denormalised output
     setting).  The loss covers sample 0 only, so the oracle runs that one
     sequence while the HIP kernels run the whole B = 4 grid.
     Bounds (bf16 storage, 30-step recurrence): output max |d| <= 5e-2, mean
-    <= 3e-3; gradients rel-L2 worst <= 0.1, median <= 3e-2.
+    <= 3e-3; gradients rel-L2 worst <= 0.1, median <= 3e-2; the scalar PReLU
+    slopes (sums of cancelling terms over 30 frames) |d| <= 0.1 x the largest
+    slope gradient.
   * cfg 5 -- mixed ACDC + DSB15 (half the volumes each, per-volume
     normalisation constants), fp16, batch 8 per GPU: EDSR on 128 slices, DUF
     on 128 seven-frame windows (loss on the first 16 samples, oracle on
@@ -42,7 +44,7 @@ def _grads(net):
     return {k: p.grad.detach().float() for k, p in net.named_parameters() if p.grad is not None}
 
 
-def _compare(mine, ref, out, rout, y, dataset, omax, omean, gworst, gmed):
+def _compare(mine, ref, out, rout, y, dataset, omax, omean, gworst, gmed, sworst=0.1):
     d = (out.detach().float() - rout.detach()).abs()
     assert d.max().item() <= omax and d.mean().item() <= omean, (d.max().item(), d.mean().item())
     p_m = psnr_denorm(out.detach().float(), y, dataset).item()
@@ -50,8 +52,16 @@ def _compare(mine, ref, out, rout, y, dataset, omax, omean, gworst, gmed):
     assert abs(p_m - p_r) <= 0.01, (p_m, p_r)
     g_m, g_r = _grads(mine), _grads(ref)
     gmax = max(v.norm().item() for v in g_r.values())
+    # A scalar PReLU slope's gradient is one sum over every voxel of a frame
+    # sequence, of terms of both signs: its 16-bit error scales with the sum
+    # of |terms|, not with the (cancelling) sum.  The slopes are held to an
+    # absolute bound on the scale of the largest slope gradient instead.
+    smax = max([v.abs().item() for v in g_r.values() if v.numel() == 1] or [0.0])
     rels = {}
     for k, gr in g_r.items():
+        if gr.numel() == 1:
+            assert (g_m[k] - gr).abs().item() <= sworst * smax, (k, g_m[k].item(), gr.item(), smax)
+            continue
         if gr.norm().item() <= 1e-6 * gmax:  # exact gradient ~0 (conv bias before a BatchNorm)
             assert g_m[k].norm().item() <= 2e-2 * gmax, k
             continue

@@ -286,32 +286,34 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     }
   };
 
-  // Epilogue operand prefetch (2-D, one operand): 4 channels (8 bytes) per
-  // (row, block, channel group), the layout of the accumulator lanes.  The
-  // loads are inline asm like the DMA pieces: the compiler's own vmcnt
-  // bookkeeping cannot see those, and would drain the in-flight stage at the
-  // first use.  They are issued before the stage's DMA pieces, so the
-  // stage wait of the next step retires them; `settle` then ties the uses
-  // after that step's barrier.
-  typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
-  u32x2_t pre[PREF ? RMS : 1][PREF ? NT : 1][4];
+  // Epilogue operand prefetch (2-D, one operand), in the transposed
+  // epilogue's layout: lane l reads 8 channels (16 bytes) 8 (l & 3) .. +7 of
+  // the block of voxel (l >> 2) + 16 k.  The loads are inline asm like the
+  // DMA pieces: the compiler's own vmcnt bookkeeping cannot see those, and
+  // would drain the in-flight stage at the first use.  The stage waits of the
+  // main loop retire them (see pf_hold); `settle` ties the uses after the
+  // flush's barrier.
+  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+  u32x4_t pre[PREF ? RMS : 1][PREF ? NT : 1][2];
   const RView& pv = (EM & RE_RES) ? a.res : a.msk;
+  const int tv = lane >> 2, tc8 = lane & 3;  // transposed roles: voxel (of 16), 8-channel group
   auto prefetch = [&](const RTile& tl, int dz) __attribute__((always_inline)) {
     if constexpr (PREF) {
 #pragma unroll
       for (int ms = 0; ms < RMS; ++ms) {
-        const int ho = tl.h0 + wave * RMS + ms, wo = tl.w0 + r;
-        const bool ok = ho < a.y.h && wo < a.y.w;
-        const H* pp = reinterpret_cast<const H*>(pv.ptr) +
-                      (tl.nb * pv.sn + dz * pv.sd + ho * pv.sh + wo * pv.sw + tl.n0 + 4 * hf);
+        const int ho = tl.h0 + wave * RMS + ms;
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
+        for (int k = 0; k < 2; ++k) {
+          const int wo = tl.w0 + tv + 16 * k;
+          const bool ok = ho < a.y.h && wo < a.y.w;
+          const H* pp = reinterpret_cast<const H*>(pv.ptr) +
+                        (tl.nb * pv.sn + dz * pv.sd + ho * pv.sh + wo * pv.sw + tl.n0 + 8 * tc8);
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const bool okc = ok && tl.n0 + nt * 32 + 8 * g + 4 * hf < a.cout;
-            const void* src = okc ? (const void*)(pp + nt * 32 + 8 * g) : (const void*)zp;
-            asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(pre[ms][nt][g]) : "v"(src) : "memory");
+          for (int nt = 0; nt < NT; ++nt) {
+            const void* src = ok ? (const void*)(pp + nt * 32) : (const void*)zp;
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(pre[ms][nt][k]) : "v"(src) : "memory");
           }
+        }
       }
     }
   };
@@ -322,7 +324,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-          for (int g = 0; g < 4; ++g) asm volatile("" : "+v"(pre[ms][nt][g]));
+          for (int k = 0; k < 2; ++k) asm volatile("" : "+v"(pre[ms][nt][k]));
     }
   };
 
@@ -423,18 +425,14 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
               for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
             }
             if constexpr (EM & RE_MASK) {
-              uint2 mv;
-              if constexpr (PREF) mv = use_pre ? __builtin_bit_cast(uint2, pre[ms][nt][g]) : *reinterpret_cast<const uint2*>(mp + 8 * g);
-              else mv = *reinterpret_cast<const uint2*>(mp + 8 * g);
+              const uint2 mv = *reinterpret_cast<const uint2*>(mp + 8 * g);
               float mm[4];
               unpack_pk<H>(mv, mm);
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] = mm[e] > 0.f ? v[e] : 0.f;
             }
             if constexpr (EM & RE_RES) {
-              uint2 rv;
-              if constexpr (PREF) rv = use_pre ? __builtin_bit_cast(uint2, pre[ms][nt][g]) : *reinterpret_cast<const uint2*>(rp + 8 * g);
-              else rv = *reinterpret_cast<const uint2*>(rp + 8 * g);
+              const uint2 rv = *reinterpret_cast<const uint2*>(rp + 8 * g);
               float rr[4];
               unpack_pk<H>(rv, rr);
 #pragma unroll
@@ -452,12 +450,95 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       }
     }
   };
+  // Transposed 2-D epilogue (output block nt of depth dz): per row ms the
+  // wave parks its fp32 accumulators (32 voxels x 32 channels) in LDS and
+  // reads them back as 8 consecutive channels of one voxel per lane, so every
+  // global access (output, residual, mask, accumulate) is 16 contiguous bytes
+  // and a wave instruction covers 16 voxels x 64 bytes -- instead of 32
+  // voxels x 8 bytes, which doubled the cost of a residual / mask operand.
+  // The scratch is the wave's own DMA pieces 0-3 of the slot the next DMA
+  // fills (free after the barrier; only this wave writes them, and only after
+  // its flush): voxel v in piece v / 8, row v % 8 (128 bytes), 16-byte column
+  // c at c ^ (v & 7) (conflict-free parking and read-back).
+  auto epilogue_tr = [&](const f32x16 (&A)[RMS], const RTile& tl, int dz, int nt, bool use_pre, char* scr)
+                         __attribute__((always_inline)) {
+    char* ws = scr + wave * 1024;
+#pragma unroll
+    for (int ms = 0; ms < RMS; ++ms) {
+      const int ho = tl.h0 + wave * RMS + ms;
+      if (ho >= a.y.h) continue;  // wave-uniform
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(ws + (r >> 3) * 8 * 1024 + (r & 7) * 128 + (((2 * g + hf) ^ (r & 7)) * 16)) =
+            make_float4(A[ms][4 * g], A[ms][4 * g + 1], A[ms][4 * g + 2], A[ms][4 * g + 3]);
+      const int co = tl.n0 + nt * 32 + 8 * tc8;
+      const float4 b0 = *reinterpret_cast<const float4*>(lbias + co);
+      const float4 b1 = *reinterpret_cast<const float4*>(lbias + co + 4);
+      const float bsv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int v = tv + 16 * k, wo = tl.w0 + v;
+        const char* rb = ws + (v >> 3) * 8 * 1024 + (v & 7) * 128;
+        const float4 q0 = *reinterpret_cast<const float4*>(rb + (((2 * tc8) ^ (v & 7)) * 16));
+        const float4 q1 = *reinterpret_cast<const float4*>(rb + (((2 * tc8 + 1) ^ (v & 7)) * 16));
+        float t[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          t[e] = fmaf(t[e], osc, bsv[e]);
+          if constexpr (EM & RE_RELU) t[e] = fmaxf(t[e], 0.f);
+        }
+        if (wo < a.y.w) {
+          H* yp = reinterpret_cast<H*>(a.y.ptr) + (tl.yo + dz * a.y.sd + (wave * RMS + ms) * a.y.sh + v * a.y.sw +
+                                                   nt * 32 + 8 * tc8);
+          if constexpr (EM & RE_MASK) {
+            uint4 mv;
+            if constexpr (PREF) {
+              if (use_pre) mv = __builtin_bit_cast(uint4, pre[ms][nt][k]);
+              else
+                mv = *reinterpret_cast<const uint4*>(reinterpret_cast<const H*>(a.msk.ptr) +
+                                                     (tl.nb * a.msk.sn + dz * a.msk.sd + ho * a.msk.sh + wo * a.msk.sw + co));
+            } else {
+              mv = *reinterpret_cast<const uint4*>(reinterpret_cast<const H*>(a.msk.ptr) +
+                                                   (tl.nb * a.msk.sn + dz * a.msk.sd + ho * a.msk.sh + wo * a.msk.sw + co));
+            }
+            float m[8];
+            Chunk<H>::unpack(mv, m);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) t[e] = m[e] > 0.f ? t[e] : 0.f;
+          }
+          if constexpr (EM & RE_RES) {
+            uint4 rv;
+            if constexpr (PREF) {
+              if (use_pre) rv = __builtin_bit_cast(uint4, pre[ms][nt][k]);
+              else
+                rv = *reinterpret_cast<const uint4*>(reinterpret_cast<const H*>(a.res.ptr) +
+                                                     (tl.nb * a.res.sn + dz * a.res.sd + ho * a.res.sh + wo * a.res.sw + co));
+            } else {
+              rv = *reinterpret_cast<const uint4*>(reinterpret_cast<const H*>(a.res.ptr) +
+                                                   (tl.nb * a.res.sn + dz * a.res.sd + ho * a.res.sh + wo * a.res.sw + co));
+            }
+            float rr[8];
+            Chunk<H>::unpack(rv, rr);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) t[e] += rr[e];
+          }
+          if constexpr (EM & RE_ACC) {
+            float o[8];
+            Chunk<H>::unpack(*reinterpret_cast<const uint4*>(yp), o);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) t[e] += o[e];
+          }
+          *reinterpret_cast<uint4*>(yp) = Chunk<H>::pack(t);
+        }
+      }
+    }
+  };
   // Flush after slice pdi of tile tl.  KD 3: the banks whose output depth
   // takes no more contributions -- dz = pdi + pd - 2 when the walk stays in
   // the tile (all = false), every bank at the end of the tile -- are stored
   // (if inside the tile's depth run) and zeroed.  KD 1: output depth pdi + pd,
   // every block.
-  auto flush = [&](const RTile& tl, int pdi, bool all, bool use_pre) __attribute__((always_inline)) {
+  auto flush = [&](const RTile& tl, int pdi, bool all, bool use_pre, char* scr) __attribute__((always_inline)) {
     const int P = pdi + a.pd;
     if constexpr (KD == 3) {
       const int bdone = (P + 1) % 3;  // bank of P - 2
@@ -475,7 +556,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     } else {
 #pragma unroll
       for (int b = 0; b < NACC; ++b) {
-        if (P >= tl.z0 && P < tl.z1) epilogue(acc[b], tl, P, b, use_pre);
+        if (P >= tl.z0 && P < tl.z1) epilogue_tr(acc[b], tl, P, b, use_pre, scr);
 #pragma unroll
         for (int m = 0; m < RMS; ++m)
 #pragma unroll
@@ -529,23 +610,43 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   int pdi = -1;     // slice whose end is still to be flushed (-1: none)
   bool pall = false;
   bool ppre = false;  // its epilogue operand was prefetched
+  // The 2-D operand prefetch of a slice is issued at the end of its third-to-
+  // last stage (chunk nchunk - 3), AFTER that stage's DMA pieces, and the two
+  // following steps wait with NPF more loads outstanding: the slice's last two
+  // stages cover its latency, as the DMA ring's two stages of lookahead do,
+  // and the step after (the flush) retires it.  Shorter slices: at chunk 0
+  // (one stage of cover), or with one chunk before the last stage's pieces.
+  constexpr int NPF = RMS * NT * 2;
+  int pf_hold = 0;         // steps whose wait leaves the prefetch in flight
+  bool pf_slice = false;   // the current slice's operand was prefetched
   // one stage; false when it was the workgroup's last
+  char* fscr = lds;  // the final flush's scratch slot: the one the last stage's DMA walk left free
   auto step = [&](auto slot_c) __attribute__((always_inline)) -> bool {
-    if (tnext) roll_wait_vmcnt<RNQ>();  // this stage landed (and any prefetch); the next stays in flight
-    else roll_wait_vmcnt<0>();
+    fscr = lds + ((decltype(slot_c)::value + 2) % 3) * RSLOT;
+    if (PREF && pf_hold > 0) {
+      --pf_hold;
+      if (tnext) roll_wait_vmcnt<RNQ + NPF>();  // this stage landed; the next stage and the prefetch stay in flight
+      else roll_wait_vmcnt<NPF>();
+    } else {
+      if (tnext) roll_wait_vmcnt<RNQ>();  // this stage landed (and any earlier prefetch); the next stays in flight
+      else roll_wait_vmcnt<0>();
+    }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // this slot ready, the previous one free
     if (pdi >= 0) {
       if (ppre) settle();
-      flush(ptl, pdi, pall, ppre);
+      flush(ptl, pdi, pall, ppre, lds + ((decltype(slot_c)::value + 2) % 3) * RSLOT);
     }
     const int di = ct.di_lo + cs;
-    // the tile's last chunk of a slice that completes a 2-D output depth:
-    // its epilogue operand is loaded now, before this stage's DMA pieces
-    ppre = false;
+    const bool out_in = di + a.pd >= ct.z0 && di + a.pd < ct.z1;  // this slice completes an output depth (2-D)
+    bool pf_next = false;
     if constexpr (PREF) {
-      if (cc == a.nchunk - 1 && di + a.pd >= ct.z0 && di + a.pd < ct.z1) {
-        prefetch(ct, di + a.pd);
-        ppre = true;
+      if (a.nchunk == 1) {
+        if (out_in) {
+          prefetch(ct, di + a.pd);
+          pf_slice = true;
+        }
+      } else if (cc == max(a.nchunk - 3, 0) && out_in) {
+        pf_next = true;
       }
     }
     Dma dn;
@@ -554,6 +655,13 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     dn.use = 0;
     if (vn) dn = prep(nx);
     compute(slot_c, di + a.pd, kd_mask(ct.z0, ct.z1, di), dn, vn, tnext, tc, tm);
+    if constexpr (PREF) {
+      if (pf_next) {
+        prefetch(ct, di + a.pd);
+        pf_slice = true;
+        pf_hold = min(2, a.nchunk - 1);
+      }
+    }
     // the stage after the next one is nx's (issued just now): it becomes "next"
     tnext = vn;
     tc = nx.c;
@@ -566,6 +674,8 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     ptl = ct;
     pdi = di;
     pall = false;
+    ppre = pf_slice;
+    pf_slice = false;
     if (++cs < ct.nsl) return true;
     cs = 0;
     pall = true;
@@ -580,7 +690,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   }
   roll_wait_vmcnt<0>();  // the last stage's prefetch
   if (ppre) settle();
-  flush(ptl, pdi, true, ppre);
+  flush(ptl, pdi, true, ppre, fscr);
 }
 
 int g_roll_mode = -1;  // -1: from VSRK_CONV_ROLL (default on), 0 off, 1 on

@@ -479,7 +479,10 @@ bool vsrk_wgrad_roll_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const 
   const int nz = ceil_div(dy->d, z);
   const int64_t nt = spatial * nz;
   if (nt >= (1ll << 30)) return false;
-  int splits = (int)std::max<int64_t>(1, std::min<int64_t>(nt, ceil_div64(want_wg, combos)));
+  // one workgroup per CU (the ring takes the whole LDS): the grid must not
+  // spill a few workgroups into a second wave (224 -> 32 with 37 x 7 = 259
+  // workgroups on 256 CUs: 6.0 ms, r3e microbench)
+  int splits = (int)std::max<int64_t>(1, std::min<int64_t>(nt, want_wg / combos));
   if (vsrk_g_grid_cap > 0) splits = std::max(1, std::min(splits, vsrk_g_grid_cap));
   const int t = (int)ceil_div64(nt, splits);
   splits = (int)ceil_div64(nt, t);
