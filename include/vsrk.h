@@ -79,7 +79,15 @@ typedef struct vsrk_conv_desc {
   const float* act_param;  /* device scalar, VSRK_ACT_PRELU: nn.PReLU(num_parameters=1) slope (drf_net.py:56) */
   const float* mask_slope; /* device scalar or NULL: where mask <= 0 the output is scaled by *mask_slope
                               instead of zeroed -- the PReLU backward dx = dy * (y > 0 ? 1 : a) */
+  int32_t subpixel;   /* 0, or VSRK_SUBPIXEL(k, s, p, transposed, flipped): the weight is the
+                         vsrk_subpixel_conv_weight image of nn.Conv2d / nn.ConvTranspose2d(k, stride s,
+                         padding p) (drf_net.py:70-102), packed with mode `flipped`, and the shuffle-s
+                         operand (x or y) carries its sub-pixel phase: taps whose weights are zero for a
+                         whole phase may be skipped (4 of 9 at k = 8, s = 4, p = 2).  Results are those
+                         of the dense weight. */
 } vsrk_conv_desc;
+#define VSRK_SUBPIXEL(k, s, p, transposed, flipped) \
+  ((int32_t)((k) | ((s) << 8) | ((p) << 16) | ((transposed) ? 1 << 24 : 0) | ((flipped) ? 1 << 25 : 0)))
 
 /* Repack an fp32 torch conv weight (cout, cin, kd, kh, kw) into the kernel
  * layout [kd][kh][kw][round_up(cout',128)][round_up(cin',32)] of `dtype`.

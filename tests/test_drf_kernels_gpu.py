@@ -45,8 +45,12 @@ def _nchw(t):  # (N,1,H,W,C) -> (N,C,H,W)
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("r", [2, 3, 4, 8])
 @pytest.mark.parametrize("f", [16, 64])
-def test_subpixel_deconv_and_conv(dtype, r, f):
+@pytest.mark.parametrize("skip", [False, True])
+def test_subpixel_deconv_and_conv(dtype, r, f, skip):
+    """skip: the sub-pixel structure is passed (F.subpixel_code), so kernels
+    that can skip each phase's zero taps do."""
     k, s, p = PROJ[r]
+    sc = (lambda tr, fl: F.subpixel_code(k, s, p, tr, fl)) if skip else (lambda tr, fl: 0)
     g = torch.Generator().manual_seed(r * 10 + f)
     n, h, w = 2, 5, 7 if r < 8 else 3
     H, W = h * s, w * s
@@ -75,17 +79,19 @@ def test_subpixel_deconv_and_conv(dtype, r, f):
     # --- transposed conv: 3x3 conv f -> s*s*f written through a shuffle-s view
     weq, beq = F.subpixel_conv_weight(wd.to(DEV), bd.to(DEV), k, s, p, transposed=True)
     out = torch.empty((n, 1, H, W, f), dtype=dtype, device=DEV)
-    F.conv(_cl(x_lr).to(DEV, dtype), F.pack_weight(weq, 0, dtype), out, K3, P1, bias=beq, y_shuffle=s, bias_r=1)
+    F.conv(_cl(x_lr).to(DEV, dtype), F.pack_weight(weq, 0, dtype), out, K3, P1, bias=beq, y_shuffle=s, bias_r=1,
+           subpixel=sc(True, False))
     ref = _cl(yd.detach())
     assert (out.double().cpu() - ref).abs().max().item() <= _tol(dtype, ref)
     g_hr = _cl(gy_hr).to(DEV, dtype)
     dx = torch.empty((n, 1, h, w, f), dtype=dtype, device=DEV)
-    F.conv(g_hr, F.pack_weight(weq, 1, dtype), dx, K3, P1, x_shuffle=s)
+    F.conv(g_hr, F.pack_weight(weq, 1, dtype), dx, K3, P1, x_shuffle=s, subpixel=sc(True, True))
     ref = _cl(xl.grad)
     assert (dx.double().cpu() - ref).abs().max().item() <= _tol(dtype, ref), "deconv dgrad"
     dweq = torch.empty_like(weq)
     dbeq = torch.empty_like(beq)
-    F.conv_wgrad(_cl(x_lr).to(DEV, dtype), g_hr, K3, P1, dweq.view(*weq.shape[:2], 1, 3, 3), dbeq, dy_shuffle=s)
+    F.conv_wgrad(_cl(x_lr).to(DEV, dtype), g_hr, K3, P1, dweq.view(*weq.shape[:2], 1, 3, 3), dbeq, dy_shuffle=s,
+                 subpixel=sc(True, False))
     dw = torch.empty_like(wd, device=DEV)
     db = torch.empty_like(bd, device=DEV)
     F.subpixel_wgrad_fold(dweq, dbeq, dw, db, k, s, p, transposed=True)
@@ -97,17 +103,18 @@ def test_subpixel_deconv_and_conv(dtype, r, f):
     weq, beq = F.subpixel_conv_weight(wc.to(DEV), bc.to(DEV), k, s, p, transposed=False)
     xh_d = _cl(x_hr).to(DEV, dtype)
     out = torch.empty((n, 1, h, w, f), dtype=dtype, device=DEV)
-    F.conv(xh_d, F.pack_weight(weq, 0, dtype), out, K3, P1, bias=beq, x_shuffle=s)
+    F.conv(xh_d, F.pack_weight(weq, 0, dtype), out, K3, P1, bias=beq, x_shuffle=s, subpixel=sc(False, False))
     ref = _cl(yc.detach())
     assert (out.double().cpu() - ref).abs().max().item() <= _tol(dtype, ref), "conv fwd"
     g_lr = _cl(gy_lr).to(DEV, dtype)
     dx = torch.empty((n, 1, H, W, f), dtype=dtype, device=DEV)
-    F.conv(g_lr, F.pack_weight(weq, 1, dtype), dx, K3, P1, y_shuffle=s, bias_r=1)
+    F.conv(g_lr, F.pack_weight(weq, 1, dtype), dx, K3, P1, y_shuffle=s, bias_r=1, subpixel=sc(False, True))
     ref = _cl(xh.grad)
     assert (dx.double().cpu() - ref).abs().max().item() <= _tol(dtype, ref), "conv dgrad"
     dweq = torch.empty_like(weq)
     dbeq = torch.empty_like(beq)
-    F.conv_wgrad(xh_d, g_lr, K3, P1, dweq.view(*weq.shape[:2], 1, 3, 3), dbeq, x_shuffle=s)
+    F.conv_wgrad(xh_d, g_lr, K3, P1, dweq.view(*weq.shape[:2], 1, 3, 3), dbeq, x_shuffle=s,
+                 subpixel=sc(False, False))
     dw = torch.empty_like(wc, device=DEV)
     db = torch.empty_like(bc, device=DEV)
     F.subpixel_wgrad_fold(dweq, dbeq, dw, db, k, s, p, transposed=False)

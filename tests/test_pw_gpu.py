@@ -81,7 +81,7 @@ def test_pw_forward_depth_slice_head_chunks(grid_cap):
 
 
 @pytest.mark.parametrize("combo", ["mask", "acc", "mask+acc"])
-@pytest.mark.parametrize("c", [128, 256])
+@pytest.mark.parametrize("c", [64, 128, 192, 256])
 def test_pw_data_gradient_epilogues(c, combo, grid_cap):
     """dgrad form (mode-1 packed weight, no prologue) with the ReLU mask of the
     forward output and / or accumulation into an existing gradient."""
@@ -205,3 +205,56 @@ def test_pw_fp16_forward_and_weight_gradient(c):
                  pro_scale=sc.to(DEV), pro_shift=sh.to(DEV))
     ew = (dw.view(c, c).double().cpu() - ref_w).abs().max().item()
     assert ew <= 2e-3 * (1 + ref_w.abs().max().item()), ew
+
+
+@pytest.mark.parametrize("ci,co", [(128, 64), (192, 64), (256, 64), (256, 16), (64, 128), (64, 192), (64, 256)])
+@pytest.mark.parametrize("form", ["plain", "prologue+relu", "prelu", "mask+acc", "prelu-mask"])
+def test_pw_non_square(ci, co, form, grid_cap):
+    """Narrowing 1x1 convs (cout < cin: DRF's feedback projections
+    Conv2d((i+1)F, F, 1) + PReLU at low and high resolution,
+    drf_net.py:81-92; DUF's residual head 256 -> 16, duf_net.py:46-49) and
+    widening ones (their data gradients F -> (i+1)F, accumulated) on the
+    staged kernel with one output chunk: channel-slice input and output
+    views, every epilogue form."""
+    g = torch.Generator().manual_seed(ci + 7 * co)
+    n, d, h, w = 2, 1, 13, 40
+    big = torch.randn((n, d, h, w, ci + 32), generator=g)
+    wt = torch.randn((co, ci), generator=g) / ci ** 0.5
+    b = torch.randn(co, generator=g)
+    sc = torch.rand(ci, generator=g) + 0.5
+    sh = torch.randn(ci, generator=g)
+    mask = torch.randn((n, d, h, w, co), generator=g)
+    y0 = torch.randn((n, d, h, w, co + 64), generator=g)
+    slope = torch.tensor([0.2])
+    xin = _q(big[..., 16:16 + ci])
+    kw = {}
+    if form == "prologue+relu":
+        xin = torch.relu(xin * sc.double() + sh.double()).to(BF).double()
+        kw = dict(bias=b.to(DEV), prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV),
+                  act=F.ACT_RELU)
+    elif form == "plain":
+        kw = dict(bias=b.to(DEV))
+    elif form == "prelu":
+        kw = dict(bias=b.to(DEV), act=F.ACT_PRELU, act_param=slope.to(DEV))
+    ref = torch.einsum("ndhwc,oc->ndhwo", xin, _q(wt))
+    if form == "plain":
+        ref = ref + b.double()
+    if form == "prelu":
+        ref = ref + b.double()
+        ref = torch.where(ref > 0, ref, 0.2 * ref)
+    if form == "prologue+relu":
+        ref = torch.relu(ref + b.double())
+    if form == "mask+acc":
+        ref = torch.where(_q(mask) > 0, ref, torch.zeros_like(ref)) + _q(y0[..., 32:32 + co])
+        kw = dict(mask=mask.to(DEV, BF), accumulate=True)
+    if form == "prelu-mask":
+        ref = torch.where(_q(mask) > 0, ref, 0.2 * ref)
+        kw = dict(mask=mask.to(DEV, BF), mask_slope=slope.to(DEV))
+    yb = y0.to(DEV, BF)
+    F.conv(big.to(DEV, BF)[..., 16:16 + ci], F.pack_weight(wt.view(co, ci, 1, 1, 1).to(DEV), 0, BF),
+           yb[..., 32:32 + co], (1, 1, 1), (0, 0, 0), **kw)
+    y = yb[..., 32:32 + co].double().cpu()
+    err = (y - ref).abs().max().item()
+    assert err <= 2 * 1.5e-2 * ref.abs().max().item(), err
+    assert torch.equal(yb[..., :32].cpu(), y0[..., :32].to(BF)) and torch.equal(yb[..., 32 + co:].cpu(),
+                                                                                 y0[..., 32 + co:].to(BF))

@@ -214,3 +214,74 @@ def test_roll_2d_tiling_invariant_and_path(epi):
     tol = _tol(torch.bfloat16, ref)
     assert (yf - ref).abs().max().item() <= tol
     assert (y0 - ref).abs().max().item() <= tol
+
+
+# ---- sub-pixel forms: DRF's projections (drf_net.py:70-102) over shuffle-s views ----
+PROJ = {2: (6, 2, 2), 4: (8, 4, 2)}
+
+
+def _run_sub(r, form, epi, skip, cap=0, roll=-1, seed=0):
+    """form "up": ConvTranspose2d as a 3x3 conv written through a shuffle-r
+    output view (forward; "down_dgrad" is the same form with a flipped
+    strided-conv weight); "down": the strided conv reading a shuffle-r input
+    view ("up_dgrad" likewise).  epi: plain / prelu / acc."""
+    k, s, p = PROJ[r]
+    f, n, h, w = 64, 2, 13, 37
+    g = torch.Generator().manual_seed(seed + r)
+    tr = form in ("up", "up_dgrad")
+    flip = form.endswith("dgrad")
+    wt = torch.randn((f, f, k, k), generator=g) / (f * k) ** 0.5
+    b = torch.randn(f, generator=g)
+    weq, beq = F.subpixel_conv_weight(wt.to(DEV), b.to(DEV), k, s, p, transposed=tr)
+    dt = torch.bfloat16
+    wp = F.pack_weight(weq, 1 if flip else 0, dt)
+    ys = form in ("up", "down_dgrad")
+    if ys:
+        x = torch.randn((n, 1, h, w, f), generator=g)
+        y0 = torch.randn((n, 1, h * s, w * s, 2 * f), generator=g)
+    else:
+        x = torch.randn((n, 1, h * s, w * s, 2 * f), generator=g)
+        y0 = torch.randn((n, 1, h, w, 2 * f), generator=g)
+    xd = x.to(DEV, dt)[..., :f] if not ys else x.to(DEV, dt)
+    yb = y0.to(DEV, dt)
+    yv = yb[..., f:]
+    slope = torch.tensor([0.25], device=DEV)
+    kw = dict(subpixel=F.subpixel_code(k, s, p, tr, flip) if skip else 0)
+    if not flip:
+        kw.update(bias=beq, bias_r=1)
+    if epi == "prelu":
+        kw.update(act=F.ACT_PRELU, act_param=slope)
+    if epi == "acc":
+        kw.update(accumulate=True)
+    F.set_grid_cap(cap)
+    F.set_conv_path("roll", roll)
+    try:
+        F.conv(xd, wp, yv, (1, 3, 3), (0, 1, 1), x_shuffle=1 if ys else s, y_shuffle=s if ys else 1, **kw)
+    finally:
+        F.set_grid_cap(0)
+        F.set_conv_path("roll", -1)
+    torch.cuda.synchronize()
+    return yb.double().cpu(), y0
+
+
+@pytest.mark.parametrize("r", [2, 4])
+@pytest.mark.parametrize("form", ["up", "down", "up_dgrad", "down_dgrad"])
+@pytest.mark.parametrize("epi", ["plain", "prelu", "acc"])
+def test_roll_subpixel_forms(r, form, epi):
+    """the rolling 2-D kernel over a shuffled operand, with and without the
+    per-phase tap skip and at capped grids, against the conv_fast path (a
+    different kernel, itself checked against fp64 in test_drf_kernels_gpu):
+    equal within one bf16 rounding; tap skipping and the grid give BITWISE
+    the same output (zero taps add exact zeros); the untouched half of the
+    output buffer stays as it was."""
+    if form.endswith("dgrad") and epi == "prelu":
+        pytest.skip("data gradients carry no activation")
+    yref, y0 = _run_sub(r, form, epi, skip=False, roll=0)
+    y, _ = _run_sub(r, form, epi, skip=True)
+    scale = max(yref.abs().max().item(), 1e-3)
+    assert (y - yref).abs().max().item() <= 1.5e-2 * scale
+    f = 64
+    assert torch.equal(y[..., :f], y0[..., :f].to(torch.bfloat16).double())
+    for skip, cap in ((False, 0), (True, 3)):
+        y2, _ = _run_sub(r, form, epi, skip=skip, cap=cap)
+        assert torch.equal(y2, y), (skip, cap)

@@ -45,6 +45,7 @@ class ConvDesc(C.Structure):
         ("bias_perm_r", C.c_int32),
         ("act_param", C.c_void_p),
         ("mask_slope", C.c_void_p),
+        ("subpixel", C.c_int32),
     ]
 
 

@@ -221,6 +221,11 @@ struct WgradArgs {
   int prologue, xvec, dyvec;
   int tiles_h, tiles_w, ntiles, tiles_per_split, nsplit, ncombos, nblk;
   int n_ci_chunks, n_co_tiles, kd_bias, slab, want_bias, cin_pad;
+  // sub-pixel weight (desc->subpixel): taps with a nonzero weight per
+  // 32-channel block of the shuffled operand (dy: sp_by 1, x: sp_by 2);
+  // the others' gradients are structurally discarded (vsrk_subpixel_wgrad_fold)
+  int sp_by;
+  uint16_t sptap[64];
 };
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
@@ -249,6 +254,28 @@ static inline bool chunk_ok(const vsrk_tensor5* t, int esize) {
   const bool stride_ok = t->sw >= epc || (t->w == 1);
   return ((uintptr_t)t->ptr) % 16 == 0 && t->sn % epc == 0 && t->sd % epc == 0 && t->sh % epc == 0 &&
          t->sw % epc == 0 && block_ok && stride_ok;
+}
+
+// Tap mask (bit kh*3 + kw of the PACKED weight) of sub-pixel phase `sub` for
+// a VSRK_SUBPIXEL(k, s, p, transposed, flipped) weight: the kernel row of tap
+// kh at phase row si is s*(kh - 1) + si + p (strided conv) or s*(1 - kh) + si
+// + p (transposed), as vsrk_subpixel_conv_weight builds it (drf.hip); a mode-1
+// packing flips the taps.  All taps when the descriptor carries no structure.
+static inline uint16_t subpixel_tapmask(int32_t code, int r, int sub) {
+  if (code == 0) return 0x1ff;
+  const int k = code & 0xff, sp = (code >> 8) & 0xff, p = (code >> 16) & 0xff;
+  const bool tr = (code >> 24) & 1, flip = (code >> 25) & 1;
+  if (sp != r) return 0x1ff;
+  const int si = sub / r, sj = sub % r;
+  auto row = [&](int tap, int ph) { return tr ? sp * (1 - tap) + ph + p : sp * (tap - 1) + ph + p; };
+  uint16_t m = 0;
+  for (int kh = 0; kh < 3; ++kh)
+    for (int kw = 0; kw < 3; ++kw) {
+      const int th = flip ? 2 - kh : kh, tw = flip ? 2 - kw : kw;
+      const int ky = row(th, si), kx = row(tw, sj);
+      if (ky >= 0 && ky < k && kx >= 0 && kx < k) m |= (uint16_t)(1u << (kh * 3 + kw));
+    }
+  return m;
 }
 
 // pipelined 16-bit 3x3(x3) weight gradient (conv_wgrad_pipe.hip): 1 = launched the slab kernel, 0 = not eligible.

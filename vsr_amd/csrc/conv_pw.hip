@@ -130,6 +130,7 @@ struct PwArgs {  // 16-bit tensors of one type H (bf16 / fp16)
   const float* pro_scale;
   const float* pro_shift;
   const float* mask_slope;
+  const float* act_param;                 // PReLU slope (device scalar)
   int64_t xsn, xsw, ysn, ysw, msn, msw;  // element strides
   int nvox, dhw;
   FastDiv fd;                             // division by dhw
@@ -323,7 +324,8 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
   }
 }
 
-// Staged variant (no mask / accumulate, NCB <= 7): each wave owns an LDS
+// Staged variant (NCB <= 7 output blocks, NKB <= 8 input blocks; NCB < NKB
+// for the narrowing 1x1 convs, e.g. DRF's 256 -> 64): each wave owns an LDS
 // tile buffer [32*M voxels][CIP + 8 pad] H.  The next tile is fetched with
 // coalesced 16-byte loads (consecutive lanes -> consecutive bytes of a voxel
 // row, then the next row) into registers while the current tile computes; the
@@ -334,15 +336,21 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
 // row's offset is row * sw from the tile's base -- the common, cheap case;
 // otherwise rows are placed with a division per row.  ACT: VSRK_ACT_NONE /
 // VSRK_ACT_RELU at compile time (the epilogue is most of the VALU work).
-template <int NCB, int M, bool PRO, bool AL, int ACT, typename H>
+// EIN: the ReLU/PReLU mask and / or accumulate of a data gradient
+// (dx = mask(conv) [+ dx]) applied on the 16-byte row chunks of the store
+// pass, their operands loaded as coalesced rows like the output (the tile
+// kernel read them 8 bytes per lane across 32 voxel rows).  The buffered
+// value is rounded to H before the accumulate: one extra rounding of the new
+// term against the tile kernel.
+template <int NCB, int NKB, int M, bool PRO, bool AL, int ACT, bool EIN, typename H>
 __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
   const H* aX = reinterpret_cast<const H*>(a.x);
   H* aY = reinterpret_cast<H*>(a.y);
   const H* aW = reinterpret_cast<const H*>(a.w);
-  constexpr int KS = 2 * NCB;
+  constexpr int KS = 2 * NKB;
   constexpr int COP = 32 * NCB;
   constexpr int CIP = 16 * KS;
-  constexpr int RS = 2 * CIP + 16;           // buffer row stride (bytes)
+  constexpr int RS = 2 * (CIP > COP ? CIP : COP) + 16;  // buffer row stride (bytes): input or output row
   constexpr int CPR = CIP / 8;               // 16-byte chunks per row
   constexpr int ROWS = 32 * M;
   constexpr int NCK = ROWS * CPR / 64;       // chunks per lane per tile (= M*KS)
@@ -373,6 +381,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
   const int nwaves = gridDim.x * (PW_THR / 64);
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   const float osc = a.out_scale;
+  const float pslope = ACT == VSRK_ACT_PRELU ? *a.act_param : 0.f;
 
   // byte offset of tile row `row` (voxel v0 + row) from the tile's sample base
   auto row_off = [&](const TileBase& tb, int row, int v0, int64_t sn, int64_t sw) __attribute__((always_inline)) {
@@ -483,6 +492,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
             for (int e = 0; e < 4; ++e) {
               o[e] *= osc;
               if constexpr (ACT == VSRK_ACT_RELU) o[e] = fmaxf(o[e], 0.f);
+              if constexpr (ACT == VSRK_ACT_PRELU) o[e] = o[e] > 0.f ? o[e] : pslope * o[e];
             }
             lds_st8(ebase + m * 32 * RS + (cb * 32 + 8 * j) * 2, pack_pk<H, uint2>(o));
           }
@@ -494,12 +504,43 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
       const Rsrc ry = rsrc_at(aY + (int64_t)tb.n0 * a.ysn);
       constexpr int OCPR = COP / 8;
       constexpr int NOK = ROWS * OCPR / 64;
+      static_assert(NOK >= 1 && ROWS * OCPR % 64 == 0, "whole row chunks per lane");
       int ln = lane;
       asm volatile("" : "+v"(ln));
+      // EIN operands of every chunk first (all loads in flight together)
+      uint4 em[EIN ? NOK : 1], ey[EIN ? NOK : 1];
+      if constexpr (EIN) {
+        const Rsrc rm = rsrc_at(reinterpret_cast<const H*>(a.has_mask ? a.msk : a.y) + (int64_t)tb.n0 * a.msn);
+#pragma unroll
+        for (int k = 0; k < NOK; ++k) {
+          const int i = ln + 64 * k, row = i / OCPR, c = 8 * (i % OCPR);
+          const bool ok = co0 + c < a.cout;
+          if (a.has_mask) em[k] = bload16(rm, ok ? row_off(tb, row, v0, a.msn, a.msw) + 2 * (co0 + c) : PW_OOB);
+          if (a.accumulate) ey[k] = bload16(ry, ok ? row_off(tb, row, v0, a.ysn, a.ysw) + 2 * (co0 + c) : PW_OOB);
+        }
+      }
+      const float mslope = (EIN && a.mask_slope) ? *a.mask_slope : 0.f;
 #pragma unroll
       for (int k = 0; k < NOK; ++k) {
         const int i = ln + 64 * k, row = i / OCPR, c = 8 * (i % OCPR);
-        const uint4 v = *reinterpret_cast<const uint4*>(buf + row * RS + c * 2);
+        uint4 v = *reinterpret_cast<const uint4*>(buf + row * RS + c * 2);
+        if constexpr (EIN) {
+          float o[8];
+          Chunk<H>::unpack(v, o);
+          if (a.has_mask) {
+            float m[8];
+            Chunk<H>::unpack(em[k], m);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = mask_apply(m[e], o[e], mslope);
+          }
+          if (a.accumulate) {
+            float yo[8];
+            Chunk<H>::unpack(ey[k], yo);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] += yo[e];
+          }
+          v = Chunk<H>::pack(o);
+        }
         const uint32_t off = row_off(tb, row, v0, a.ysn, a.ysw);
         if (!(a.ablate & 1))
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), ry,
@@ -773,43 +814,71 @@ static bool dhw_dense(const vsrk_tensor5* t) {
          (t->d == 1 || t->sd == (int64_t)t->h * t->sh);
 }
 
-template <int NCB, int M, typename H>
-static void launch_fwd(const PwArgs& a, int nchunk, bool pro, hipStream_t s) {
-  constexpr int KS = 2 * NCB, COP = 32 * NCB, CIP = 16 * KS;
-  int grid = (int)std::min<int64_t>(pw_num_cus(), ceil_div64(a.ntiles, PW_THR / 64));
-  if (vsrk_g_grid_cap > 0) grid = std::min(grid, vsrk_g_grid_cap);
-  grid = std::max(grid, 1);
-  const bool ein = a.has_mask || a.accumulate;
-  if constexpr (NCB <= 7) {
-    static int staged = -1;
-    if (staged < 0) {
-      const char* e = getenv("VSRK_PW_STAGED");
-      staged = (e && e[0] == '0') ? 0 : 1;
-    }
-    if (!ein && staged && a.cout % 8 == 0) {
-      const size_t lds =
-          (size_t)KS * 2 * COP * 16 + (pro ? 2 * CIP * 4 : 0) + COP * 4 + 4 * (32 * M) * (2 * CIP + 16);
-      const bool al = a.dhw % (32 * M) == 0;
-      const bool relu = a.act == VSRK_ACT_RELU;
-      using K = void (*)(PwArgs);
-      K kern;
-      if (pro) {
-        if (al) kern = relu ? pw_fwd_staged_kernel<NCB, M, true, true, 1, H> : pw_fwd_staged_kernel<NCB, M, true, true, 0, H>;
-        else kern = relu ? pw_fwd_staged_kernel<NCB, M, true, false, 1, H> : pw_fwd_staged_kernel<NCB, M, true, false, 0, H>;
-      } else {
-        if (al) kern = relu ? pw_fwd_staged_kernel<NCB, M, false, true, 1, H> : pw_fwd_staged_kernel<NCB, M, false, true, 0, H>;
-        else kern = relu ? pw_fwd_staged_kernel<NCB, M, false, false, 1, H> : pw_fwd_staged_kernel<NCB, M, false, false, 0, H>;
-      }
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      kern<<<dim3(grid, nchunk), PW_THR, lds, s>>>(a);
-      return;
-    }
+// Staged launch (LDS row buffers) of (NCB output blocks, NKB input blocks);
+// false when the staged kernel is off (VSRK_PW_STAGED=0) or the output is
+// not 8-channel aligned.
+template <int NCB, int NKB, int M, typename H>
+static bool launch_fwd_staged(const PwArgs& a, int grid, int nchunk, bool pro, hipStream_t s) {
+  constexpr int KS = 2 * NKB, COP = 32 * NCB, CIP = 16 * KS;
+  static int staged = -1;
+  if (staged < 0) {
+    const char* e = getenv("VSRK_PW_STAGED");
+    staged = (e && e[0] == '0') ? 0 : 1;
   }
+  if (!staged || a.cout % 8 != 0) return false;
+  const bool ein = a.has_mask || a.accumulate;
+  if (ein && (pro || a.act != VSRK_ACT_NONE)) return false;  // data gradients: no prologue / activation
+  if (pro && a.act == VSRK_ACT_PRELU) return false;
+  constexpr int RW = CIP > COP ? CIP : COP;
+  const size_t lds = (size_t)KS * 2 * COP * 16 + (pro ? 2 * CIP * 4 : 0) + COP * 4 + 4 * (32 * M) * (2 * RW + 16);
+  const bool al = a.dhw % (32 * M) == 0;
+  const bool relu = a.act == VSRK_ACT_RELU;
+  using K = void (*)(PwArgs);
+  K kern;
+  if (ein) {
+    kern = al ? pw_fwd_staged_kernel<NCB, NKB, M, false, true, 0, true, H>
+              : pw_fwd_staged_kernel<NCB, NKB, M, false, false, 0, true, H>;
+  } else if (a.act == VSRK_ACT_PRELU) {
+    kern = al ? pw_fwd_staged_kernel<NCB, NKB, M, false, true, VSRK_ACT_PRELU, false, H>
+              : pw_fwd_staged_kernel<NCB, NKB, M, false, false, VSRK_ACT_PRELU, false, H>;
+  } else if (pro) {
+    if (al) kern = relu ? pw_fwd_staged_kernel<NCB, NKB, M, true, true, 1, false, H>
+                        : pw_fwd_staged_kernel<NCB, NKB, M, true, true, 0, false, H>;
+    else kern = relu ? pw_fwd_staged_kernel<NCB, NKB, M, true, false, 1, false, H>
+                     : pw_fwd_staged_kernel<NCB, NKB, M, true, false, 0, false, H>;
+  } else {
+    if (al) kern = relu ? pw_fwd_staged_kernel<NCB, NKB, M, false, true, 1, false, H>
+                        : pw_fwd_staged_kernel<NCB, NKB, M, false, true, 0, false, H>;
+    else kern = relu ? pw_fwd_staged_kernel<NCB, NKB, M, false, false, 1, false, H>
+                     : pw_fwd_staged_kernel<NCB, NKB, M, false, false, 0, false, H>;
+  }
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  kern<<<dim3(grid, nchunk), PW_THR, lds, s>>>(a);
+  return true;
+}
+
+static int pw_grid(int64_t ntiles) {
+  int grid = (int)std::min<int64_t>(pw_num_cus(), ceil_div64(ntiles, PW_THR / 64));
+  if (vsrk_g_grid_cap > 0) grid = std::min(grid, vsrk_g_grid_cap);
+  return std::max(grid, 1);
+}
+
+// false: not launched (a PReLU activation needs the staged kernel)
+template <int NCB, int M, typename H>
+static bool launch_fwd(const PwArgs& a, int nchunk, bool pro, hipStream_t s) {
+  constexpr int KS = 2 * NCB, COP = 32 * NCB, CIP = 16 * KS;
+  const int grid = pw_grid(a.ntiles);
+  if constexpr (NCB <= 7) {
+    if (launch_fwd_staged<NCB, NCB, M, H>(a, grid, nchunk, pro, s)) return true;
+  }
+  if (a.act == VSRK_ACT_PRELU) return false;
+  const bool ein = a.has_mask || a.accumulate;
   const size_t lds = (size_t)KS * 2 * COP * 16 + (2 * CIP + COP) * sizeof(float);
   auto kern = pro ? (ein ? pw_fwd_kernel<NCB, M, true, true, H> : pw_fwd_kernel<NCB, M, true, false, H>)
                   : (ein ? pw_fwd_kernel<NCB, M, false, true, H> : pw_fwd_kernel<NCB, M, false, false, H>);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   kern<<<dim3(grid, nchunk), PW_THR, lds, s>>>(a);
+  return true;
 }
 
 // tiles of 32*M voxels, M chosen so one wave step loads ~16 KiB
@@ -825,7 +894,8 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
   if (!pw_enabled()) return 0;
   if (!vsrk_is16(x->dtype) || y->dtype != x->dtype) return 0;
   if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->pd || d->ph || d->pw) return 0;
-  if (residual || d->act == VSRK_ACT_PRELU || d->bias_perm_r > 1) return 0;
+  if (residual || d->bias_perm_r > 1) return 0;
+  if (d->act == VSRK_ACT_PRELU && !d->act_param) return 0;
   if (x->n != y->n || x->d != y->d || x->h != y->h || x->w != y->w) return 0;
   if (!dhw_dense(x) || !dhw_dense(y) || (mask && (!dhw_dense(mask) || mask->dtype != x->dtype))) return 0;
   if (mask && (mask->n != y->n || mask->d != y->d || mask->h != y->h || mask->w != y->w || mask->c != y->c)) return 0;
@@ -836,8 +906,14 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
   const int ncb = cip / 32;  // square kernels: COP = CIP
   if (ncb < 2 || ncb > 8) return 0;
   const int cop_total = round_up(y->c, 32);
-  if (cop_total % cip != 0) return 0;  // output handled in chunks of CIP channels
-  const int nchunk = cop_total / cip;
+  // narrowing convs (DRF's 128..256 -> 64 projections, DUF's 256 -> 16
+  // residual head) and the widening data gradients of DRF's 64 -> 128..256
+  // projections: one output chunk of cop_total != cip channels (one pass
+  // over x instead of cop_total / cip)
+  const bool wide_ok = ncb == 2 && (cop_total == 128 || cop_total == 192 || cop_total == 256);
+  const int narrow = (cop_total < cip || wide_ok) ? cop_total / 32 : 0;
+  if (!narrow && cop_total % cip != 0) return 0;  // output handled in chunks of CIP channels
+  const int nchunk = narrow ? 1 : cop_total / cip;
   PwArgs a;
   a.x = x->ptr;
   a.y = y->ptr;
@@ -847,6 +923,7 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
   a.pro_scale = pro_scale;
   a.pro_shift = pro_shift;
   a.mask_slope = d->mask_slope;
+  a.act_param = d->act_param;
   a.xsn = x->sn; a.xsw = x->sw;
   a.ysn = y->sn; a.ysw = y->sw;
   a.msn = mask ? mask->sn : 0;
@@ -880,14 +957,43 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
   a.out_scale = d->out_scale;
   if (a.nvox == 0) return 1;
   const bool pro = d->prologue != VSRK_PRO_NONE;
+  if (narrow) {
+    bool ok = false;
+    auto go = [&](auto ncb_c, auto nkb_c) {
+      constexpr int NC = decltype(ncb_c)::value, NK = decltype(nkb_c)::value;
+      constexpr int M = pw_m<NK>() * NC <= 8 ? pw_m<NK>() : (8 / NC > 0 ? 8 / NC : 1);  // <= 128 accumulators
+      a.ntiles = ceil_div(a.nvox, 32 * M);
+      vsrk_dispatch16(x->dtype, [&](auto tag) {
+        ok = launch_fwd_staged<NC, NK, M, decltype(tag)>(a, pw_grid(a.ntiles), 1, pro, s);
+        return 0;
+      });
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    if (narrow == 1 && ncb == 8) go(I1{}, std::integral_constant<int, 8>{});
+    else if (narrow == 2 && ncb == 4) go(I2{}, std::integral_constant<int, 4>{});
+    else if (narrow == 2 && ncb == 6) go(I2{}, std::integral_constant<int, 6>{});
+    else if (narrow == 2 && ncb == 8) go(I2{}, std::integral_constant<int, 8>{});
+    else if (narrow == 4 && ncb == 2) go(std::integral_constant<int, 4>{}, I2{});
+    else if (narrow == 6 && ncb == 2) go(std::integral_constant<int, 6>{}, I2{});
+    else if (narrow == 8 && ncb == 2) go(std::integral_constant<int, 8>{}, I2{});
+    else return 0;
+    if (!ok) return 0;
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      vsrk_set_error("conv_fwd_pw: launch failed: %s", hipGetErrorString(e));
+      return -(int)VSRK_ERR_LAUNCH;
+    }
+    return 1;
+  }
   switch (ncb) {
 #define PW_CASE(N)                                                     \
   case N:                                                              \
     a.ntiles = ceil_div(a.nvox, 32 * pw_m<N>());                       \
-    vsrk_dispatch16(x->dtype, [&](auto tag) {                          \
-      launch_fwd<N, pw_m<N>(), decltype(tag)>(a, nchunk, pro, s);      \
+    if (!vsrk_dispatch16(x->dtype, [&](auto tag) {                     \
+          return (int)launch_fwd<N, pw_m<N>(), decltype(tag)>(a, nchunk, pro, s); \
+        }))                                                            \
       return 0;                                                        \
-    });                                                                \
     break;
     PW_CASE(2) PW_CASE(3) PW_CASE(4) PW_CASE(5) PW_CASE(6) PW_CASE(7) PW_CASE(8)
 #undef PW_CASE

@@ -31,6 +31,14 @@
 // Tile: 8 waves x 2 rows x 32 columns x 32 output channels x a run of output
 // depths [z0, z1) of one sample.  MFMA v_mfma_f32_32x32x16_{bf16,f16},
 // operands "weights x voxels" (a lane's accumulator column is one voxel).
+//
+// Sub-pixel forms (2-D only, SP = 1 / 2): DRF's strided Conv2d /
+// ConvTranspose2d(k, s, p) projections run as 3x3 convs on the low-res grid
+// over a shuffle-s input (SP 1) or output (SP 2) view (drf_net.py:70-102,
+// vsrk_subpixel_conv_weight).  Each sub-pixel phase of the shuffled operand
+// meets only a 2 x 2 (k = 2s) window of the 3 x 3 taps; the other taps' weights
+// are structurally zero and their MFMAs are skipped (a per-phase tap mask:
+// 4 of 9 taps at k = 8, s = 4, p = 2).
 #include <cstdlib>
 #include "conv_common.h"
 
@@ -67,8 +75,11 @@ struct RollGeo {
 };
 
 // Epilogue forms (compile time): out = fma(acc, out_scale, bias*out_scale)
-// [relu] [* (mask > 0)] [+ residual] [+ out]
-enum { RE_RES = 1, RE_MASK = 2, RE_ACC = 4, RE_RELU = 8 };
+// [relu | prelu] [* (mask > 0)] [+ residual] [+ out]
+enum { RE_RES = 1, RE_MASK = 2, RE_ACC = 4, RE_RELU = 8, RE_PRELU = 16 };
+// sub-pixel operand (2-D forms): none, input view, output view
+enum { SP_NONE = 0, SP_X = 1, SP_Y = 2 };
+constexpr int RMAXSUB = 64;  // chunk / block table entries (1024 logical channels)
 
 // Division by a launch constant d (dividends < 2^31): q = (x * mul) >> p with
 // p = 31 + ceil(log2 d), mul = ceil(2^p / d).
@@ -102,6 +113,12 @@ struct RollArgs {
   float out_scale;
   int dzc, nchunk, ntiles;
   RDiv ntn, nzc, tiles_w, tiles_h;
+  // sub-pixel forms: per input chunk (SP_X) / 32-channel output block (SP_Y),
+  // the element offset of its channels inside the shuffled operand (phase
+  // row / column + physical channel) and its tap mask (bit kh*3 + kw)
+  const float* act_param;
+  int spoff[RMAXSUB];
+  uint16_t sptap[RMAXSUB];
 };
 
 __device__ __attribute__((aligned(256))) uint4 g_roll_zero[16];
@@ -112,8 +129,9 @@ __device__ __forceinline__ void roll_wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int KD, int NT, int PRO, int EM, typename H>
+template <int KD, int NT, int PRO, int EM, int SP, typename H>
 __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
+  static_assert(SP == SP_NONE || KD == 1, "sub-pixel views: 2-D form only");
   using G = RollGeo<KD, NT>;
   constexpr int RNQ = G::NQ, RSLOT = G::SLOT, NACC = G::NACC;
   // the residual / mask operand of a 2-D tile is loaded into registers during
@@ -199,7 +217,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     tl.di_lo = max(0, tl.z0 - a.pd);
     tl.nsl = min(a.x.d - 1, tl.z1 + KD - 2 - a.pd) - tl.di_lo + 1;
     tl.xo = nb * a.x.sn + (tl.h0 - a.ph) * a.x.sh + (tl.w0 - a.pw) * a.x.sw;
-    tl.yo = nb * a.y.sn + tl.h0 * a.y.sh + tl.w0 * a.y.sw + tl.n0;
+    tl.yo = nb * a.y.sn + tl.h0 * a.y.sh + tl.w0 * a.y.sw + (SP == SP_Y ? 0 : tl.n0);
     return tl;
   };
   // spatial validity of this lane's A pieces for a tile (bit q)
@@ -252,7 +270,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     Dma d;
     const int di = k.tl.di_lo + k.sl;
     const int c0 = k.c * RCH;
-    d.xb = reinterpret_cast<const H*>(a.x.ptr) + (k.tl.xo + di * a.x.sd + c0);
+    d.xb = reinterpret_cast<const H*>(a.x.ptr) + (k.tl.xo + di * a.x.sd + (SP == SP_X ? a.spoff[k.c] : c0));
     d.wsrc = reinterpret_cast<const H*>(a.w) + (k.tl.n0 * a.cin_pad + c0);
     const unsigned km = kd_mask(k.tl.z0, k.tl.z1, di);
     d.use = (k.m & qa) | ((km & 1) ? qkd0 : 0u) | ((km & 2) ? qkd1 : 0u) | ((km & 4) ? qkd2 : 0u);
@@ -338,7 +356,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // this wave's A pieces of the NEXT stage (slot SLOT+1, landed one stage
   // ago), beside the MFMAs instead of in front of the barrier.
   auto compute = [&](auto slot_c, int P, unsigned km, const Dma& dn, bool don, bool tnext, int tc,
-                     unsigned tm) __attribute__((always_inline)) {
+                     unsigned tm, unsigned tk0, unsigned tk1) __attribute__((always_inline)) {
     constexpr int SLOT = decltype(slot_c)::value;
     const char* sl = lds + SLOT * RSLOT;
     char* sl1 = lds + ((SLOT + 1) % 3) * RSLOT;
@@ -386,10 +404,14 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
         }
       }
       if ((bm >> b) & 1) {
+        const unsigned tkb = b == 0 ? tk0 : tk1;  // sub-pixel forms: taps of this set's phase
 #pragma unroll
-        for (int kh = 0; kh < 3; ++kh)
+        for (int kh = 0; kh < 3; ++kh) {
+          if (SP == SP_NONE || ((tkb >> (kh * 3 + kw)) & 1)) {
 #pragma unroll
-          for (int ms = 0; ms < RMS; ++ms) mma<H>(acc[b][ms], bw[g & 1][kh], ax[kw & 1][ms + kh]);
+            for (int ms = 0; ms < RMS; ++ms) mma<H>(acc[b][ms], bw[g & 1][kh], ax[kw & 1][ms + kh]);
+          }
+        }
       }
     }
   };
@@ -397,6 +419,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // Epilogue of one finished output depth dz of a tile, output block nt:
   // 4 channels (8 bytes) per lane and channel group.
   const float osc = a.out_scale;
+  const float pslope = (EM & RE_PRELU) ? *a.act_param : 0.f;
   auto epilogue = [&](const f32x16 (&A)[RMS], const RTile& tl, int dz, int nt, bool use_pre)
                       __attribute__((always_inline)) {
 #pragma unroll
@@ -486,10 +509,11 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
         for (int e = 0; e < 8; ++e) {
           t[e] = fmaf(t[e], osc, bsv[e]);
           if constexpr (EM & RE_RELU) t[e] = fmaxf(t[e], 0.f);
+          if constexpr (EM & RE_PRELU) t[e] = t[e] > 0.f ? t[e] : pslope * t[e];
         }
         if (wo < a.y.w) {
           H* yp = reinterpret_cast<H*>(a.y.ptr) + (tl.yo + dz * a.y.sd + (wave * RMS + ms) * a.y.sh + v * a.y.sw +
-                                                   nt * 32 + 8 * tc8);
+                                                   (SP == SP_Y ? a.spoff[(tl.n0 >> 5) + nt] : nt * 32) + 8 * tc8);
           if constexpr (EM & RE_MASK) {
             uint4 mv;
             if constexpr (PREF) {
@@ -654,7 +678,13 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     dn.wsrc = nullptr;
     dn.use = 0;
     if (vn) dn = prep(nx);
-    compute(slot_c, di + a.pd, kd_mask(ct.z0, ct.z1, di), dn, vn, tnext, tc, tm);
+    unsigned tk0 = 0x1ffu, tk1 = 0x1ffu;
+    if constexpr (SP == SP_X) tk0 = tk1 = a.sptap[cc];
+    if constexpr (SP == SP_Y) {
+      tk0 = a.sptap[ct.n0 >> 5];
+      tk1 = a.sptap[(ct.n0 >> 5) + 1];
+    }
+    compute(slot_c, di + a.pd, kd_mask(ct.z0, ct.z1, di), dn, vn, tnext, tc, tm, tk0, tk1);
     if constexpr (PREF) {
       if (pf_next) {
         prefetch(ct, di + a.pd);
@@ -705,14 +735,15 @@ int roll_num_cus() {
   return n;
 }
 
-template <int KD, int NT, int PRO, int EM, typename H>
+template <int KD, int NT, int PRO, int EM, int SP, typename H>
 int launch_roll(const RollArgs& a, size_t lds, int grid, hipStream_t s) {
-  auto kern = conv_roll_kernel<KD, NT, PRO, EM, H>;
+  auto kern = conv_roll_kernel<KD, NT, PRO, EM, SP, H>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   kern<<<grid, RNW * 64, lds, s>>>(a);
   VSRK_LAUNCH_CHECK("conv_fwd(roll)");
   return VSRK_OK;
 }
+
 
 }  // namespace
 
@@ -742,14 +773,26 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   // depth-1 slices with 64-channel output blocks (cout a multiple of 64)
   const bool k3 = d->kd == 3;
   if (!k3 && !(d->kd == 1 && d->pd == 0 && y->c % 64 == 0)) return 0;
-  if (d->bias_perm_r > 1 || d->act == VSRK_ACT_PRELU || d->mask_slope) return 0;
+  if (d->bias_perm_r > 1 || d->mask_slope) return 0;
+  if (d->act == VSRK_ACT_PRELU && (k3 || !d->act_param)) return 0;
   if (k3 && (residual || mask || d->accumulate)) return 0;
-  if (x->shuffle > 1 || y->shuffle > 1) return 0;
+  // sub-pixel operands (2-D only, one of x / y): each 16-channel input chunk
+  // (x) or 32-channel output block (y) must lie inside one phase
+  const int sp = x->shuffle > 1 ? SP_X : (y->shuffle > 1 ? SP_Y : SP_NONE);
+  if (x->shuffle > 1 && y->shuffle > 1) return 0;
+  if (sp != SP_NONE) {
+    if (k3 || d->prologue || residual || mask) return 0;
+    const vsrk_tensor5* t = sp == SP_X ? x : y;
+    const int r = t->shuffle, cph = t->c / (r * r);
+    if (cph * r * r != t->c || cph % (sp == SP_X ? RCH : 32) != 0) return 0;
+    if (t->c / (sp == SP_X ? RCH : 32) > RMAXSUB) return 0;
+  }
   if (x->c % RCH != 0 || !chunk_ok(x, 2)) return 0;
   if (d->pd < 0 || d->pd > 2 || d->ph < 0 || d->ph > 2 || d->pw < 0 || d->pw > 2) return 0;
   if (y->d != x->d + 2 * d->pd - (d->kd - 1) || y->h != x->h + 2 * d->ph - 2 || y->w != x->w + 2 * d->pw - 2) return 0;
   auto out_ok = [&](const vsrk_tensor5* t) {  // 8-byte epilogue accesses, the output's geometry
-    return t->dtype == y->dtype && t->shuffle <= 1 && t->n == y->n && t->d == y->d && t->h == y->h && t->w == y->w &&
+    return t->dtype == y->dtype && (t->shuffle <= 1 || (t == y && sp == SP_Y)) && t->n == y->n && t->d == y->d &&
+           t->h == y->h && t->w == y->w &&
            t->c == y->c && ((uintptr_t)t->ptr) % 8 == 0 && t->sn % 4 == 0 && t->sd % 4 == 0 && t->sh % 4 == 0 &&
            t->sw % 4 == 0;
   };
@@ -757,15 +800,20 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   if ((residual && !out_ok(residual)) || (mask && !out_ok(mask))) return 0;
   for (const vsrk_tensor5* t : {x, y, residual, mask}) {  // every element offset fits in 32 bits
     if (!t) continue;
-    const int64_t span = (int64_t)(t->n - 1) * t->sn + (int64_t)(t->d - 1) * t->sd + (int64_t)(t->h - 1) * t->sh +
-                         (int64_t)(t->w - 1) * t->sw + t->c + 2 * (int64_t)RHW * t->sw + (RFTH + 2) * t->sh;
+    const int64_t r = t->shuffle > 1 ? t->shuffle : 1;
+    const int64_t span = (int64_t)(t->n - 1) * t->sn + (int64_t)(t->d - 1) * t->sd +
+                         (int64_t)(r * (t->h + RFTH + 2) - 1) * t->sh + (int64_t)(r * (t->w + 2 * RHW) - 1) * t->sw +
+                         t->c;
     if (span >= (1ll << 31) || t->sn < 0 || t->sd < 0 || t->sh < 0 || t->sw < 0) return 0;
   }
+  // a shuffled view walks the low-res grid: its row / column strides are r
+  // physical rows / columns (the phase lives in the channel offset table)
   auto rview = [](const vsrk_tensor5* t) {
     RView v;
+    const int r = t->shuffle > 1 ? t->shuffle : 1;
     v.ptr = (char*)t->ptr;
     v.d = t->d; v.h = t->h; v.w = t->w;
-    v.sn = (int)t->sn; v.sd = (int)t->sd; v.sh = (int)t->sh; v.sw = (int)t->sw;
+    v.sn = (int)t->sn; v.sd = (int)t->sd; v.sh = (int)(r * t->sh); v.sw = (int)(r * t->sw);
     return v;
   };
   RollArgs a;
@@ -787,6 +835,16 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   a.prologue = d->prologue;
   a.out_scale = d->out_scale;
   a.nchunk = x->c / RCH;
+  a.act_param = d->act_param;
+  if (sp != SP_NONE) {
+    const vsrk_tensor5* t = sp == SP_X ? x : y;
+    const int r = t->shuffle, cph = t->c / (r * r), step = sp == SP_X ? RCH : 32;
+    for (int i = 0; i < t->c / step; ++i) {
+      const int c = i * step, sub = c / cph, cc = c - sub * cph;
+      a.spoff[i] = (int)((sub / r) * t->sh + (sub % r) * t->sw + cc);
+      a.sptap[i] = subpixel_tapmask(d->subpixel, r, sub);
+    }
+  }
   const int nt = k3 ? 1 : 2;
   const int tiles_h = ceil_div(y->h, RFTH), tiles_w = ceil_div(y->w, TW), ntn = ceil_div(y->c, 32 * nt);
   const int64_t spatial = (int64_t)y->n * tiles_h * tiles_w * ntn;
@@ -819,23 +877,41 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   if (lds > 160 * 1024) return 0;
   const int grid = (int)vsrk_capped_grid(std::min<int64_t>(ntiles, roll_num_cus()));
   const bool relu = d->act == VSRK_ACT_RELU;
-  const int em = (residual ? RE_RES : 0) | (mask ? RE_MASK : 0) | (d->accumulate ? RE_ACC : 0) | (relu ? RE_RELU : 0);
+  const int em = (residual ? RE_RES : 0) | (mask ? RE_MASK : 0) | (d->accumulate ? RE_ACC : 0) | (relu ? RE_RELU : 0) |
+                 (d->act == VSRK_ACT_PRELU ? RE_PRELU : 0);
   int rc = vsrk_dispatch16(x->dtype, [&](auto tag) {
     using H = decltype(tag);
     if (k3) {
-      if (d->prologue) return relu ? launch_roll<3, 1, 1, RE_RELU, H>(a, lds, grid, s) : launch_roll<3, 1, 1, 0, H>(a, lds, grid, s);
-      return relu ? launch_roll<3, 1, 0, RE_RELU, H>(a, lds, grid, s) : launch_roll<3, 1, 0, 0, H>(a, lds, grid, s);
+      if (d->prologue) return relu ? launch_roll<3, 1, 1, RE_RELU, SP_NONE, H>(a, lds, grid, s) : launch_roll<3, 1, 1, 0, SP_NONE, H>(a, lds, grid, s);
+      return relu ? launch_roll<3, 1, 0, RE_RELU, SP_NONE, H>(a, lds, grid, s) : launch_roll<3, 1, 0, 0, SP_NONE, H>(a, lds, grid, s);
     }
     // 2-D forms of the EDSR body and its backward: plain, ReLU, residual,
     // ReLU mask, residual + accumulate (with or without the BN prologue: none
-    // of EDSR's convs has one, the generic path serves it)
+    // of EDSR's convs has one, the generic path serves it); DRF's sub-pixel
+    // projections: plain, PReLU, accumulate over a shuffled input or output
     if (d->prologue) return (int)VSRK_ERR_UNSUPPORTED;
+    if (sp == SP_X) {
+      switch (em) {
+        case 0: return launch_roll<1, 2, 0, 0, SP_X, H>(a, lds, grid, s);
+        case RE_PRELU: return launch_roll<1, 2, 0, RE_PRELU, SP_X, H>(a, lds, grid, s);
+        case RE_ACC: return launch_roll<1, 2, 0, RE_ACC, SP_X, H>(a, lds, grid, s);
+        default: return (int)VSRK_ERR_UNSUPPORTED;
+      }
+    }
+    if (sp == SP_Y) {
+      switch (em) {
+        case 0: return launch_roll<1, 2, 0, 0, SP_Y, H>(a, lds, grid, s);
+        case RE_PRELU: return launch_roll<1, 2, 0, RE_PRELU, SP_Y, H>(a, lds, grid, s);
+        case RE_ACC: return launch_roll<1, 2, 0, RE_ACC, SP_Y, H>(a, lds, grid, s);
+        default: return (int)VSRK_ERR_UNSUPPORTED;
+      }
+    }
     switch (em) {
-      case 0: return launch_roll<1, 2, 0, 0, H>(a, lds, grid, s);
-      case RE_RELU: return launch_roll<1, 2, 0, RE_RELU, H>(a, lds, grid, s);
-      case RE_RES: return launch_roll<1, 2, 0, RE_RES, H>(a, lds, grid, s);
-      case RE_MASK: return launch_roll<1, 2, 0, RE_MASK, H>(a, lds, grid, s);
-      case RE_RES | RE_ACC: return launch_roll<1, 2, 0, RE_RES | RE_ACC, H>(a, lds, grid, s);
+      case 0: return launch_roll<1, 2, 0, 0, SP_NONE, H>(a, lds, grid, s);
+      case RE_RELU: return launch_roll<1, 2, 0, RE_RELU, SP_NONE, H>(a, lds, grid, s);
+      case RE_RES: return launch_roll<1, 2, 0, RE_RES, SP_NONE, H>(a, lds, grid, s);
+      case RE_MASK: return launch_roll<1, 2, 0, RE_MASK, SP_NONE, H>(a, lds, grid, s);
+      case RE_RES | RE_ACC: return launch_roll<1, 2, 0, RE_RES | RE_ACC, SP_NONE, H>(a, lds, grid, s);
       default: return (int)VSRK_ERR_UNSUPPORTED;
     }
   });

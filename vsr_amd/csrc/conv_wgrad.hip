@@ -470,6 +470,16 @@ extern "C" int vsrk_conv_wgrad(const vsrk_conv_desc* d, const vsrk_tensor5* x, c
   a.slab = p.slab;
   a.want_bias = dbias != nullptr;
   a.cin_pad = round_up(x->c, 32 * p.nci);
+  a.sp_by = 0;
+  if (d->subpixel && d->kd == 1 && d->kh == 3 && d->kw == 3 && ((x->shuffle > 1) != (dy->shuffle > 1))) {
+    const vsrk_tensor5* t = dy->shuffle > 1 ? dy : x;
+    const int r = t->shuffle, cph = t->c / (r * r);
+    if (cph % 32 == 0 && t->c / 32 <= 64) {
+      a.sp_by = dy->shuffle > 1 ? 1 : 2;
+      const int32_t code = d->subpixel & ~(1 << 25);  // gradients of the forward (unflipped) taps
+      for (int b = 0; b < t->c / 32; ++b) a.sptap[b] = subpixel_tapmask(code, r, b * 32 / cph);
+    }
+  }
   if (p.ntiles == 0) return VSRK_OK;
   const bool vec = a.xvec && a.dyvec;
   if (vsrk_is16(x->dtype) && vsrk_conv_wgrad_thin(a, p.nco, p.nci, perm_r, x->dtype, s)) {

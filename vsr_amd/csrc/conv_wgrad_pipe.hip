@@ -128,6 +128,9 @@ __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) vo
   const int kdi = combo / a.n_ci_chunks;
   const int co0 = cot * 32 * NCO, ci0 = cic * 32 * NCI;
   const bool do_bias = a.want_bias && cic == 0 && kdi == a.kd_bias;
+  // taps of this wave's channel block pair that carry a weight (sub-pixel
+  // forms: DRF's projections, 4 of 9; the rest stay zero in the slab)
+  const unsigned tmk = a.sp_by == 1 ? a.sptap[(co0 >> 5) + cos_] : (a.sp_by == 2 ? a.sptap[(ci0 >> 5) + cis] : 0x1ffu);
 
   // ---- launch-fixed per-thread chunk roles ----
   const int yrem = tid % YCPV, xrem = tid % XCPV;
@@ -380,7 +383,8 @@ __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) vo
           const int r = xr - khi;
           if (r >= 0 && r < ROWS) {
 #pragma unroll
-            for (int kwi = 0; kwi < KK; ++kwi) mma<T>(acc[khi * KK + kwi], fa[r][c], fb[kwi]);
+            for (int kwi = 0; kwi < KK; ++kwi)
+              if ((tmk >> (khi * KK + kwi)) & 1) mma<T>(acc[khi * KK + kwi], fa[r][c], fb[kwi]);
           }
         }
       }

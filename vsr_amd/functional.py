@@ -146,12 +146,18 @@ class WeightPacker:
         return self.out
 
 
+def subpixel_code(k: int, s: int, p: int, transposed: bool, flipped: bool) -> int:
+    """VSRK_SUBPIXEL (include/vsrk.h): the sub-pixel structure of a
+    subpixel_conv_weight image packed with mode `flipped` (1 = data gradient)."""
+    return k | (s << 8) | (p << 16) | ((1 << 24) if transposed else 0) | ((1 << 25) if flipped else 0)
+
+
 def _desc(k, pad, prologue=PRO_NONE, act=ACT_NONE, out_scale=1.0, accumulate=False, bias_r=1,
-          act_param=None, mask_slope=None) -> N.ConvDesc:
+          act_param=None, mask_slope=None, subpixel=0) -> N.ConvDesc:
     kd, kh, kw = k
     pd, ph, pw = pad
     return N.ConvDesc(kd, kh, kw, pd, ph, pw, prologue, act, float(out_scale), 1 if accumulate else 0, bias_r,
-                      N.ptr(act_param), N.ptr(mask_slope))
+                      N.ptr(act_param), N.ptr(mask_slope), int(subpixel))
 
 
 def conv(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, *, bias: torch.Tensor | None = None,
@@ -159,17 +165,19 @@ def conv(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, *, bias: to
          act: int = ACT_NONE, out_scale: float = 1.0, accumulate: bool = False,
          residual: torch.Tensor | None = None, mask: torch.Tensor | None = None,
          x_shuffle: int = 1, y_shuffle: int = 1, act_param: torch.Tensor | None = None,
-         mask_slope: torch.Tensor | None = None, bias_r: int | None = None) -> torch.Tensor:
+         mask_slope: torch.Tensor | None = None, bias_r: int | None = None, subpixel: int = 0) -> torch.Tensor:
     """y[...] = epilogue(conv(prologue(x), W) + bias); writes into the given y view.
 
     residual/mask are views with y's logical shape (and y_shuffle addressing).
     act=ACT_PRELU reads its slope from the device scalar act_param; with
     mask_slope the mask keeps mask_slope * value where mask <= 0 (PReLU
     backward) instead of zero (ReLU backward).  bias_r overrides the bias
-    order (default: torch pixel-shuffle order of a y_shuffle output)."""
+    order (default: torch pixel-shuffle order of a y_shuffle output).
+    subpixel: subpixel_code(...) of a subpixel_conv_weight image (its zero
+    taps per phase may be skipped)."""
     lib = _lib()
     br = bias_r if bias_r is not None else (y_shuffle if bias is not None else 1)
-    d = _desc(k, pad, prologue, act, out_scale, accumulate, br, act_param, mask_slope)
+    d = _desc(k, pad, prologue, act, out_scale, accumulate, br, act_param, mask_slope, subpixel)
     xv = N.t5(x, x_shuffle)
     yv = N.t5(y, y_shuffle)
     rv = N.t5(residual, y_shuffle) if residual is not None else None
@@ -187,10 +195,12 @@ def conv(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, *, bias: to
 def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, k, pad, dw: torch.Tensor, dbias: torch.Tensor | None = None, *,
                prologue: int = PRO_NONE, pro_scale: torch.Tensor | None = None,
                pro_shift: torch.Tensor | None = None, dy_scale: float = 1.0, perm_r: int = 1,
-               accumulate: bool = False, x_shuffle: int = 1, dy_shuffle: int = 1) -> None:
-    """dw (fp32, torch layout) [+]= dy_scale * dL/dW; dbias likewise."""
+               accumulate: bool = False, x_shuffle: int = 1, dy_shuffle: int = 1, subpixel: int = 0) -> None:
+    """dw (fp32, torch layout) [+]= dy_scale * dL/dW; dbias likewise.
+    subpixel: subpixel_code(...) of the forward weight; only the taps that
+    weight carries per phase are computed (the others come out zero)."""
     lib = _lib()
-    d = _desc(k, pad, prologue)
+    d = _desc(k, pad, prologue, subpixel=subpixel)
     xv = N.t5(x, x_shuffle)
     gv = N.t5(dy, dy_shuffle)
     assert dw.dtype == torch.float32 and dw.is_contiguous()

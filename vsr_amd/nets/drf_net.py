@@ -214,7 +214,7 @@ class _DRFBase(BaseNet):
                     t1s[i], dec, dpr = src, up.deconv2, up.prelu2
                 wq, bq = sp(dec, True)
                 F.conv(src, wq, Hc[..., i * f:(i + 1) * f], K3, P1, bias=bq, bias_r=1, y_shuffle=s, act=PR,
-                       act_param=dpr.weight)
+                       act_param=dpr.weight, subpixel=F.subpixel_code(k, s, p, True, False))
                 if i == 0:
                     hsrc, cv, cpr = Hc[..., :f], dn.conv, dn.prelu
                 else:
@@ -224,7 +224,7 @@ class _DRFBase(BaseNet):
                     t2s[i], cv, cpr = hsrc, dn.conv2, dn.prelu2
                 wq, bq = sp(cv, False)
                 F.conv(hsrc, wq, L[..., (i + 1) * f:(i + 2) * f], K3, P1, bias=bq, x_shuffle=s, act=PR,
-                       act_param=cpr.weight)
+                       act_param=cpr.weight, subpixel=F.subpixel_code(k, s, p, False, False))
             X0n = new(h, w, 2 * f)
             ffeat = X0n[..., f:]  # f_features = next frame's hidden state (drf_net.py:45)
             F.conv(L[..., f:], pw(fb.out_block.conv), ffeat, K1, P0, bias=fb.out_block.conv.bias, act=PR,
@@ -299,10 +299,11 @@ class _DRFBase(BaseNet):
             def run():  # on the side stream: the sub-pixel wgrad and its fold
                 dweq = torch.empty((cop, cip, 1, 3, 3), dtype=torch.float32, device=dev)
                 dbeq = torch.empty(cop, dtype=torch.float32, device=dev)
+                spc = F.subpixel_code(k_, s_, p_, transposed, False)
                 if transposed:
-                    F.conv_wgrad(x, dy, K3, P1, dweq, dbeq, dy_shuffle=s_)
+                    F.conv_wgrad(x, dy, K3, P1, dweq, dbeq, dy_shuffle=s_, subpixel=spc)
                 else:
-                    F.conv_wgrad(x, dy, K3, P1, dweq, dbeq, x_shuffle=s_)
+                    F.conv_wgrad(x, dy, K3, P1, dweq, dbeq, x_shuffle=s_, subpixel=spc)
                 F.subpixel_wgrad_fold(dweq, dbeq, dw, db, k_, s_, p_, transposed, accumulate=acc)
 
             self._on_wgrad_stream(run, x, dy)
@@ -345,10 +346,11 @@ class _DRFBase(BaseNet):
                 hsrc = Hc[..., :f] if i == 0 else rc["t2s"][i]
                 sp_wgrad(cv, hsrc, gl, transposed=False)
                 wq1, _ = sp(cv, False, 1)
+                spc = F.subpixel_code(k, s, p, False, True)
                 if i == 0:
-                    F.conv(gl, wq1, dHc[..., :f], K3, P1, y_shuffle=s, accumulate=True)
+                    F.conv(gl, wq1, dHc[..., :f], K3, P1, y_shuffle=s, accumulate=True, subpixel=spc)
                 else:
-                    dt2 = F.conv(gl, wq1, new(H, W, f), K3, P1, y_shuffle=s)
+                    dt2 = F.conv(gl, wq1, new(H, W, f), K3, P1, y_shuffle=s, subpixel=spc)
                     prelu(rc["t2s"][i], dt2, dn.prelu1, dt2)
                     wgrad(dn.conv1, Hc[..., :(i + 1) * f], dt2, K1, P0)
                     F.conv(dt2, pw(dn.conv1, 1), dHc[..., :(i + 1) * f], K1, P0, accumulate=True)
@@ -359,10 +361,11 @@ class _DRFBase(BaseNet):
                 src = L[..., :f] if i == 0 else rc["t1s"][i]
                 sp_wgrad(dec, src, gh, transposed=True)
                 wq1, _ = sp(dec, True, 1)
+                spc = F.subpixel_code(k, s, p, True, True)
                 if i == 0:
-                    F.conv(gh, wq1, dL[..., :f], K3, P1, x_shuffle=s, accumulate=True)
+                    F.conv(gh, wq1, dL[..., :f], K3, P1, x_shuffle=s, accumulate=True, subpixel=spc)
                 else:
-                    dt1 = F.conv(gh, wq1, new(h, w, f), K3, P1, x_shuffle=s)
+                    dt1 = F.conv(gh, wq1, new(h, w, f), K3, P1, x_shuffle=s, subpixel=spc)
                     prelu(rc["t1s"][i], dt1, up.prelu1, dt1)
                     wgrad(up.conv1, L[..., :(i + 1) * f], dt1, K1, P0)
                     F.conv(dt1, pw(up.conv1, 1), dL[..., :(i + 1) * f], K1, P0, accumulate=True)
