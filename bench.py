@@ -394,6 +394,13 @@ def worker(args, world, rank, local):
                 rf = results[m]["roofline"]
                 if rf["achieved"]:
                     rf["frac_of_measured_peak"] = rf["achieved"] / pk["mfma_bf16_tflops"]
+        if "duf" in results:
+            # BASELINE.json north_star: ">= 50 % of CDNA4 bf16 MFMA roofline on the
+            # 3x3x3 conv fwd+bwd at batch 4x16x128x128" -- the DUF line's roofline
+            rf = results["duf"]["roofline"]
+            out["north_star"] = {"model": "duf", "kernel": rf["kernel"], "achieved": rf["achieved"],
+                                 "peak": rf["peak"], "unit": rf["unit"], "frac": rf["frac"], "target_frac": 0.5,
+                                 "frac_of_measured_peak": rf.get("frac_of_measured_peak")}
         if world == 1 and not args.no_cpu_baseline:
             for m in names:
                 results[m]["cpu_baseline"] = cpu_baseline(m)

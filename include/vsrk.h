@@ -113,6 +113,39 @@ int vsrk_conv_fwd(const vsrk_conv_desc* desc, const vsrk_tensor5* x, const void*
                   const vsrk_tensor5* residual, const vsrk_tensor5* mask,
                   const vsrk_tensor5* y, void* stream);
 
+/* A pointwise (1x1x1) conv with a per-channel reduction of its stored output
+ * fused into the store pass (DUF's dense units, duf_net.py:198-200):
+ *   mode 1 (conv1 with the BN1+ReLU prologue): out_a = sum y, out_b = sum y^2
+ *          -- the statistics of the following BatchNorm3d (bn2);
+ *   mode 2 (the data gradient of conv1, no prologue): with dy' = y * (bnx *
+ *          scale + shift > 0) and xhat = (bnx - mean) * invstd, out_a =
+ *          sum dy', out_b = sum dy' * xhat -- vsrk_bn_relu_bwd_reduce of bn1
+ *          without a second pass over y.
+ * Square convs (cin = cout, 64..224 channels), no activation / mask /
+ * residual / accumulate; VSRK_ERR_UNSUPPORTED otherwise (the caller runs
+ * vsrk_conv_fwd + the separate reduction).  Fixed-order partials
+ * (deterministic); workspace vsrk_conv_fwd_reduce_workspace() bytes. */
+size_t vsrk_conv_fwd_reduce_workspace(void);
+int vsrk_conv_fwd_reduce(const vsrk_conv_desc* desc, const vsrk_tensor5* x, const void* w_packed,
+                         const float* bias, const float* pro_scale, const float* pro_shift,
+                         const vsrk_tensor5* y, int32_t mode, const vsrk_tensor5* bnx, const float* scale,
+                         const float* shift, const float* mean, const float* invstd, float* out_a,
+                         float* out_b, void* workspace, size_t workspace_bytes, void* stream);
+
+/* A 3x3 conv's output followed by the backward of the PReLU whose gradient
+ * it is (DRF's projection chains, drf_net.py:81-102: the data gradient of a
+ * ConvTranspose2d / strided Conv2d feeding the preceding conv1's PReLU):
+ *   y = conv(x) * (y_fwd > 0 ? 1 : a),   *da [+]= sum_{y_fwd < 0} y * y_fwd / a^2
+ * with a = *desc->mask_slope and y_fwd the PReLU's forward output (y's shape
+ * and strides).  The rolling 2-D kernel's forms only (3x3 pad 1 over 64-channel
+ * output blocks, plain or sub-pixel views); VSRK_ERR_UNSUPPORTED otherwise
+ * (the caller runs vsrk_conv_fwd + vsrk_prelu_bwd).  Fixed-order partials
+ * (deterministic); workspace vsrk_conv_prelu_bwd_workspace() bytes. */
+size_t vsrk_conv_prelu_bwd_workspace(void);
+int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* desc, const vsrk_tensor5* x, const void* w_packed,
+                            const float* bias, const vsrk_tensor5* y_fwd, const vsrk_tensor5* y, float* da,
+                            int32_t accumulate_da, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Tuning knob for A/B measurement: -1 (default) = bf16 fast path when
  * eligible (env VSRK_CONV_FAST=0 disables), 0 = always the generic kernel,
  * 1 = fast path when eligible.  Results agree within bf16 rounding. */

@@ -258,3 +258,55 @@ def test_pw_non_square(ci, co, form, grid_cap):
     assert err <= 2 * 1.5e-2 * ref.abs().max().item(), err
     assert torch.equal(yb[..., :32].cpu(), y0[..., :32].to(BF)) and torch.equal(yb[..., 32 + co:].cpu(),
                                                                                  y0[..., 32 + co:].to(BF))
+
+
+@pytest.mark.parametrize("c", [64, 96, 160, 224])
+@pytest.mark.parametrize("mode", ["stats", "bn_backward"])
+def test_pw_fused_reduce(c, mode, grid_cap):
+    """vsrk_conv_fwd_reduce: DUF's conv1 with bn2's statistics fused into the
+    store pass (duf_net.py:198-201), and its data gradient with bn1's
+    BN+ReLU backward reduce fused (duf_net.py:198-200), on the dense-unit
+    views (a depth window of a channel slice of the concat buffer).  The
+    output equals the unfused conv bitwise; the sums match the separate
+    reduction kernels within fp32 summation-order noise."""
+    g = torch.Generator().manual_seed(c + (1 if mode == "stats" else 2))
+    n, D, h, w = 2, 5, 9, 37
+    big = torch.randn((n, D, h, w, c + 32), generator=g).to(DEV, BF)
+    R = big[:, 1:4, :, :, :c]
+    wt = (torch.randn((c, c, 1, 1, 1), generator=g) / c ** 0.5).to(DEV)
+    b = torch.randn(c, generator=g).to(DEV)
+    sc = (torch.rand(c, generator=g) + 0.5).to(DEV)
+    sh = torch.randn(c, generator=g).to(DEV)
+    if mode == "stats":
+        x, wp = R, F.pack_weight(wt, 0, BF)
+        kw = dict(bias=b, prologue=F.PRO_AFFINE_RELU, pro_scale=sc, pro_shift=sh)
+    else:
+        x, wp = torch.randn((n, 3, h, w, c), generator=g).to(DEV, BF), F.pack_weight(wt, 1, BF)
+        kw = {}
+        st = torch.stack([sc, sh, torch.randn(c, generator=g).to(DEV) * 0.1, (torch.rand(c, generator=g) + 0.5).to(DEV)])
+    y_ref = torch.empty((n, 3, h, w, c), dtype=BF, device=DEV)
+    F.conv(x, wp, y_ref, (1, 1, 1), (0, 0, 0), **kw)
+    y = torch.empty_like(y_ref)
+    if mode == "stats":
+        red = F.conv_reduce(x, wp, y, **kw)
+        ref = F.bn_stats(y_ref)
+    else:
+        red = F.conv_reduce(x, wp, y, bnx=R, st=st)
+        ref = F.bn_relu_bwd_reduce(R, y_ref, st)
+    assert red is not None
+    assert torch.equal(y, y_ref)
+    err = (red - ref).abs().max().item()
+    assert err <= 1e-5 * (1 + ref.abs().max().item()), err
+    # deterministic: the same launch twice gives the same sums bitwise
+    y2 = torch.empty_like(y)
+    red2 = F.conv_reduce(x, wp, y2, **kw) if mode == "stats" else F.conv_reduce(x, wp, y2, bnx=R, st=st)
+    assert torch.equal(red, red2)
+
+
+def test_pw_fused_reduce_unsupported_shape_launches_nothing():
+    """256 channels (no staged square kernel) -> None, y untouched."""
+    x = torch.randn((1, 1, 4, 8, 256)).to(DEV, BF)
+    y = torch.full((1, 1, 4, 8, 256), 3.0, dtype=BF, device=DEV)
+    wp = F.pack_weight(torch.randn((256, 256, 1, 1, 1), device=DEV), 1, BF)
+    assert F.conv_reduce(x, wp, y, bnx=x, st=torch.ones((4, 256), device=DEV)) is None
+    assert (y == 3.0).all()

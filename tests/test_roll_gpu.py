@@ -148,7 +148,7 @@ CASES2D = [
     (1, 3, 9, 35, 64, 128),
     (2, 1, 33, 70, 64, 64),
 ]
-EPI = ["plain", "relu", "res", "mask", "res_acc"]
+EPI = ["plain", "relu", "res", "mask", "res_acc", "pro"]
 
 
 def _run2d(case, dtype, epi, cap=0, roll=-1, seed=0):
@@ -161,7 +161,12 @@ def _run2d(case, dtype, epi, cap=0, roll=-1, seed=0):
     msk = torch.randn((n, d, h, w, co), generator=g)
     old = torch.randn((n, d, h, w, co), generator=g)
     scale = 0.5 if epi in ("res", "mask") else 1.0
-    ref = _ref(_q(x, dtype), _q(wt, dtype), b.double(), (0, 1, 1)) * scale
+    sc = torch.rand(ci, generator=g) + 0.5
+    sh = torch.randn(ci, generator=g)
+    xin = _q(x, dtype)
+    if epi == "pro":  # DUF's tail: BN-affine + ReLU prologue (duf_net.py:116-118)
+        xin = torch.relu(xin * sc.double() + sh.double()).to(dtype).double()
+    ref = _ref(xin, _q(wt, dtype), b.double(), (0, 1, 1)) * scale
     if epi == "relu":
         ref = torch.relu(ref)
     if epi == "mask":
@@ -180,6 +185,8 @@ def _run2d(case, dtype, epi, cap=0, roll=-1, seed=0):
         kw["residual"] = res.to(DEV, dtype)
     if epi == "res_acc":
         kw["accumulate"] = True
+    if epi == "pro":
+        kw.update(prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV))
     F.set_grid_cap(cap)
     F.set_conv_path("roll", roll)
     try:
@@ -285,3 +292,52 @@ def test_roll_subpixel_forms(r, form, epi):
     for skip, cap in ((False, 0), (True, 3)):
         y2, _ = _run_sub(r, form, epi, skip=skip, cap=cap)
         assert torch.equal(y2, y), (skip, cap)
+
+
+@pytest.mark.parametrize("form", ["up_dgrad", "down_dgrad", "plain"])
+@pytest.mark.parametrize("acc", [False, True])
+def test_roll_prelu_bwd_fused(form, acc):
+    """vsrk_conv_fwd_prelu_bwd: the data gradient of a DRF projection with the
+    backward of the PReLU before it in the epilogue (drf_net.py:81-102) --
+    against the conv followed by the separate prelu_bwd kernel: the output
+    within one bf16 rounding (the fused form rounds once), the slope
+    gradient within fp32 summation noise; twice the same launch is bitwise
+    equal."""
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(11 + (form == "plain"))
+    f, n, h, w, r = 64, 2, 13, 37, 4
+    if form == "plain":
+        x = torch.randn((n, 1, h, w, f), generator=g).to(DEV, dt)
+        wt = torch.randn((f, f, 1, 3, 3), generator=g) / (9 * f) ** 0.5
+        wp, kw, yshape = F.pack_weight(wt.to(DEV), 1, dt), {}, (n, 1, h, w, f)
+    else:
+        k, s, p = PROJ[r]
+        tr = form == "up_dgrad"
+        wt = torch.randn((f, f, k, k), generator=g) / (f * k) ** 0.5
+        weq, _ = F.subpixel_conv_weight(wt.to(DEV), None, k, s, p, transposed=tr)
+        wp = F.pack_weight(weq, 1, dt)
+        code = F.subpixel_code(k, s, p, tr, True)
+        if tr:  # x: high-res gradient through a shuffle-r view -> low-res
+            x = torch.randn((n, 1, h * s, w * s, f), generator=g).to(DEV, dt)
+            kw, yshape = dict(x_shuffle=s, subpixel=code), (n, 1, h, w, f)
+        else:   # low-res gradient -> high-res through the output view
+            x = torch.randn((n, 1, h, w, f), generator=g).to(DEV, dt)
+            kw, yshape = dict(y_shuffle=s, subpixel=code), (n, 1, h * s, w * s, f)
+    y_fwd = torch.randn(yshape, generator=g).to(DEV, dt)
+    a = torch.tensor([0.2], device=DEV)
+    da0 = torch.tensor([0.5], device=DEV)
+    y_ref = torch.empty(yshape, dtype=dt, device=DEV)
+    F.conv(x, wp, y_ref, (1, 3, 3), (0, 1, 1), **kw)
+    da_ref = da0.clone()
+    F.prelu_bwd(y_fwd, y_ref, a, y_ref, da_ref, acc)
+    outs = []
+    for _ in range(2):
+        y = torch.empty(yshape, dtype=dt, device=DEV)
+        da = da0.clone()
+        assert F.conv_prelu_bwd(x, wp, y, (1, 3, 3), (0, 1, 1), y_fwd, a, da, acc, **kw)
+        outs.append((y, da))
+    y, da = outs[0]
+    assert torch.equal(outs[1][0], y) and torch.equal(outs[1][1], da)
+    scale = y_ref.float().abs().max().item()
+    assert (y.float() - y_ref.float()).abs().max().item() <= 1e-2 * scale
+    assert abs(da.item() - da_ref.item()) <= 1e-3 * (1 + abs(da_ref.item()))

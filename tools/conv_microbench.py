@@ -17,8 +17,14 @@ CASES = {
     # the bench's DUF unit convs: 64 windows x 7 frames
     "duf64": (64, 7, 128, 128, 64, 32, (3, 3, 3), (1, 1, 1)),
     "duf224v": (64, 7, 128, 128, 224, 32, (3, 3, 3), (0, 1, 1)),
+    # the bench's three depth-valid DUF units (T = 7: 7 -> 5, 5 -> 3, 3 -> 1 depths)
+    "duf_u3": (64, 7, 128, 128, 160, 32, (3, 3, 3), (0, 1, 1)),
+    "duf_u4": (64, 5, 128, 128, 192, 32, (3, 3, 3), (0, 1, 1)),
+    "duf_u5": (64, 3, 128, 128, 224, 32, (3, 3, 3), (0, 1, 1)),
     "duf1x1x1": (64, 7, 128, 128, 128, 128, (1, 1, 1), (0, 0, 0)),
     "duf1x1x1_224": (64, 3, 128, 128, 224, 224, (1, 1, 1), (0, 0, 0)),
+    "duf1x1x1_160": (64, 7, 128, 128, 160, 160, (1, 1, 1), (0, 0, 0)),
+    "duf1x1x1_192": (64, 5, 128, 128, 192, 192, (1, 1, 1), (0, 0, 0)),
     "duf1x1x1_64": (64, 7, 128, 128, 64, 64, (1, 1, 1), (0, 0, 0)),
     # EDSR tail conv F -> 1 at HR (thin-channel kernels: fwd = thin-out, dgrad = thin-in)
     "tail": (64, 1, 512, 512, 64, 1, (1, 3, 3), (0, 1, 1)),

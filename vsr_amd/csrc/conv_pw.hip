@@ -131,6 +131,14 @@ struct PwArgs {  // 16-bit tensors of one type H (bf16 / fp16)
   const float* pro_shift;
   const float* mask_slope;
   const float* act_param;                 // PReLU slope (device scalar)
+  // fused per-channel reduction of the stored output (RED 1: BatchNorm
+  // statistics sum y, sum y^2; RED 2: BatchNorm+ReLU backward sum dy',
+  // sum dy' xhat with dy' = y * (bnx * scale + shift > 0), xhat =
+  // (bnx - mean) * invstd): per-lane partials, slab [block][wave][lane][16]
+  const void* bnx;
+  int64_t bsn, bsw;
+  const float *bsc, *bsh, *bmu, *bis;
+  float* red_ws;
   int64_t xsn, xsw, ysn, ysw, msn, msw;  // element strides
   int nvox, dhw;
   FastDiv fd;                             // division by dhw
@@ -342,7 +350,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
 // kernel read them 8 bytes per lane across 32 voxel rows).  The buffered
 // value is rounded to H before the accumulate: one extra rounding of the new
 // term against the tile kernel.
-template <int NCB, int NKB, int M, bool PRO, bool AL, int ACT, bool EIN, typename H>
+template <int NCB, int NKB, int M, bool PRO, bool AL, int ACT, bool EIN, typename H, int RED = 0>
 __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
   const H* aX = reinterpret_cast<const H*>(a.x);
   H* aY = reinterpret_cast<H*>(a.y);
@@ -382,6 +390,25 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   const float osc = a.out_scale;
   const float pslope = ACT == VSRK_ACT_PRELU ? *a.act_param : 0.f;
+  // fused reduction: this lane's fixed 8-channel column and its constants
+  constexpr int ROCPR = COP / 8;
+  constexpr int RSTEP = 64 / ROCPR > 0 ? 64 / ROCPR : 1;
+  constexpr int RNIT = RED ? (ROWS + RSTEP - 1) / RSTEP : 1;
+  const int rcol = lane % ROCPR, rrow0 = lane / ROCPR;
+  const bool rch_ok = co0 + 8 * rcol < a.cout;
+  float rs1[8], rs2[8], rsc[8], rsh[8], rmu[8], ris[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    rs1[e] = rs2[e] = 0.f;
+    rsc[e] = rsh[e] = rmu[e] = ris[e] = 0.f;
+    if constexpr (RED == 2) {
+      const int c = min(co0 + 8 * rcol + e, a.cout - 1);
+      rsc[e] = a.bsc[c];
+      rsh[e] = a.bsh[c];
+      rmu[e] = a.bmu[c];
+      ris[e] = a.bis[c];
+    }
+  }
 
   // byte offset of tile row `row` (voxel v0 + row) from the tile's sample base
   auto row_off = [&](const TileBase& tb, int row, int v0, int64_t sn, int64_t sw) __attribute__((always_inline)) {
@@ -498,7 +525,57 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
           }
         }
     }
-    {
+    if constexpr (RED != 0) {
+      // reduce form of the store pass: lane l keeps ONE 8-channel column
+      // (l % OCPR) and walks rows l / OCPR + RSTEP j, so its partial sums
+      // are per channel; the lanes past OCPR * RSTEP idle
+      const int v0 = t * ROWS;
+      const TileBase tb = tile_base(v0, a.fd);
+      const Rsrc ry = rsrc_at(aY + (int64_t)tb.n0 * a.ysn);
+      const Rsrc rb = rsrc_at(reinterpret_cast<const H*>(RED == 2 ? a.bnx : a.y) + (int64_t)tb.n0 * a.bsn);
+      const bool lane_ok = lane < ROCPR * RSTEP;
+      uint4 bx[RNIT];
+      if constexpr (RED == 2) {
+#pragma unroll
+        for (int j = 0; j < RNIT; ++j) {
+          const int row = rrow0 + RSTEP * j;
+          const bool ok = lane_ok && row < ROWS && rch_ok;
+          bx[j] = bload16(rb, ok ? row_off(tb, row, v0, a.bsn, a.bsw) + 2 * (co0 + 8 * rcol) : PW_OOB);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < RNIT; ++j) {
+        const int row = rrow0 + RSTEP * j;
+        if (lane_ok && row < ROWS) {
+          const uint4 v = *reinterpret_cast<const uint4*>(buf + row * RS + 16 * rcol);
+          const uint32_t off = row_off(tb, row, v0, a.ysn, a.ysw);
+          const bool vox_ok = AL || v0 + row < a.nvox;
+          if (!(a.ablate & 1))
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), ry,
+                                                   (int)(rch_ok ? off + 2 * (co0 + 8 * rcol) : PW_OOB), 0, 0);
+          if (vox_ok && rch_ok) {
+            float o[8];
+            Chunk<H>::unpack(v, o);  // the stored (rounded) values, as the separate pass reads them
+            if constexpr (RED == 1) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                rs1[e] += o[e];
+                rs2[e] = fmaf(o[e], o[e], rs2[e]);
+              }
+            } else {
+              float xb[8];
+              Chunk<H>::unpack(bx[j], xb);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const float dy = fmaf(xb[e], rsc[e], rsh[e]) > 0.f ? o[e] : 0.f;
+                rs1[e] += dy;
+                rs2[e] = fmaf(dy, (xb[e] - rmu[e]) * ris[e], rs2[e]);
+              }
+            }
+          }
+        }
+      }
+    } else {
       const int v0 = t * ROWS;
       const TileBase tb = tile_base(v0, a.fd);
       const Rsrc ry = rsrc_at(aY + (int64_t)tb.n0 * a.ysn);
@@ -549,6 +626,64 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
     }
     t = tn;
   }
+  if constexpr (RED != 0) {
+    float* o = a.red_ws + ((((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (PW_THR / 64) + wave) * 64 + lane) * 16;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] = rs1[e];
+      o[8 + e] = rs2[e];
+    }
+  }
+}
+
+// Channel c of a fused reduction: sum of the lane partials that hold its
+// column, over (block, wave, lane) in a fixed order, in double.
+__global__ __launch_bounds__(256) void pw_red_final_kernel(const float* __restrict__ ws, int nbx, int cop, int ocpr,
+                                                           int rstep, int cout, float* __restrict__ o1,
+                                                           float* __restrict__ o2) {
+  const int c = blockIdx.x;
+  if (c >= cout) return;
+  const int yc = c / cop, cc = c - yc * cop, col = cc >> 3, e = cc & 7;
+  const int nlane = rstep;            // lanes of column col: col + ocpr * k, k < rstep
+  const int nitems = nbx * (PW_THR / 64) * nlane;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = threadIdx.x; i < nitems; i += 256) {
+    const int k = i % nlane, bw = i / nlane;  // bw = block * waves + wave
+    const float* p = ws + (((int64_t)yc * nbx * (PW_THR / 64) + bw) * 64 + col + ocpr * k) * 16;
+    s1 += p[e];
+    s2 += p[8 + e];
+  }
+  __shared__ double r1[256], r2[256];
+  r1[threadIdx.x] = s1;
+  r2[threadIdx.x] = s2;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) {
+      r1[threadIdx.x] += r1[threadIdx.x + k];
+      r2[threadIdx.x] += r2[threadIdx.x + k];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    o1[c] = (float)r1[0];
+    o2[c] = (float)r2[0];
+  }
+}
+
+// Staged launch with the fused per-channel reduction (square f -> f convs,
+// one output chunk): RED 1 with the BN prologue (a BatchNorm's input
+// statistics, duf_net.py:198-201), RED 2 without (the data gradient that
+// feeds a BN+ReLU backward, duf_net.py:198-200).
+template <int NCB, int M, int RED, typename H>
+static bool launch_fwd_reduce(const PwArgs& a, int grid, hipStream_t s) {
+  constexpr int KS = 2 * NCB, COP = 32 * NCB, CIP = 16 * KS;
+  const size_t lds = (size_t)KS * 2 * COP * 16 + (RED == 1 ? 2 * CIP * 4 : 0) + COP * 4 + 4 * (32 * M) * (2 * CIP + 16);
+  const bool al = a.dhw % (32 * M) == 0;
+  auto kern = al ? pw_fwd_staged_kernel<NCB, NCB, M, RED == 1, true, 0, false, H, RED>
+                 : pw_fwd_staged_kernel<NCB, NCB, M, RED == 1, false, 0, false, H, RED>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  kern<<<dim3(grid, 1), PW_THR, lds, s>>>(a);
+  return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -887,6 +1022,55 @@ constexpr int pw_m() { return NCB <= 2 ? 4 : (NCB <= 4 ? 2 : 1); }
 
 }  // namespace
 
+// The forward / data-gradient arguments common to every staged and tile
+// pointwise launch; false when a lane offset could pass 2 GiB.
+static bool pw_fill_args(PwArgs& a, const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed,
+                         const float* bias, const float* pro_scale, const float* pro_shift, const vsrk_tensor5* mask,
+                         const vsrk_tensor5* y, int cip) {
+  a = PwArgs{};
+  a.x = x->ptr;
+  a.y = y->ptr;
+  a.msk = mask ? mask->ptr : nullptr;
+  a.w = w_packed;
+  a.bias = bias;
+  a.pro_scale = pro_scale;
+  a.pro_shift = pro_shift;
+  a.mask_slope = d->mask_slope;
+  a.act_param = d->act_param;
+  a.xsn = x->sn; a.xsw = x->sw;
+  a.ysn = y->sn; a.ysw = y->sw;
+  a.msn = mask ? mask->sn : 0;
+  a.msw = mask ? mask->sw : 0;
+  a.dhw = x->d * x->h * x->w;
+  const int64_t nvox = (int64_t)x->n * a.dhw;
+  if (nvox >= (1ll << 31) - 4096) return false;
+  a.nvox = (int)nvox;
+  a.fd = make_fastdiv(std::max(a.dhw, 1));
+  {
+    // lane offsets relative to a tile's first sample stay below 2 GiB
+    const int64_t span_n = 32 * 4 / std::max(a.dhw, 1) + 2;
+    for (const vsrk_tensor5* t : {x, y, mask}) {
+      if (t && 2 * (span_n * t->sn + (int64_t)a.dhw * t->sw + t->c) >= 0x7FFFFFF0ll) return false;
+    }
+  }
+  static int ablate = -1;
+  if (ablate < 0) {
+    const char* e = getenv("VSRK_PW_ABLATE");
+    ablate = e ? atoi(e) : 0;
+  }
+  a.ablate = ablate;
+  a.cin = x->c;
+  a.cout = y->c;
+  a.ci_pad = cip;
+  a.co_rows = round_up(y->c, 128);
+  a.prologue = d->prologue;
+  a.act = d->act;
+  a.accumulate = d->accumulate;
+  a.has_mask = mask != nullptr;
+  a.out_scale = d->out_scale;
+  return true;
+}
+
 // 1 = launched, 0 = not eligible (caller uses the tile kernels), <0 = -status.
 int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
                      const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
@@ -915,46 +1099,7 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
   if (!narrow && cop_total % cip != 0) return 0;  // output handled in chunks of CIP channels
   const int nchunk = narrow ? 1 : cop_total / cip;
   PwArgs a;
-  a.x = x->ptr;
-  a.y = y->ptr;
-  a.msk = mask ? mask->ptr : nullptr;
-  a.w = w_packed;
-  a.bias = bias;
-  a.pro_scale = pro_scale;
-  a.pro_shift = pro_shift;
-  a.mask_slope = d->mask_slope;
-  a.act_param = d->act_param;
-  a.xsn = x->sn; a.xsw = x->sw;
-  a.ysn = y->sn; a.ysw = y->sw;
-  a.msn = mask ? mask->sn : 0;
-  a.msw = mask ? mask->sw : 0;
-  a.dhw = x->d * x->h * x->w;
-  const int64_t nvox = (int64_t)x->n * a.dhw;
-  if (nvox >= (1ll << 31) - 4096) return 0;
-  a.nvox = (int)nvox;
-  a.fd = make_fastdiv(std::max(a.dhw, 1));
-  {
-    // lane offsets relative to a tile's first sample stay below 2 GiB
-    const int64_t span_n = 32 * 4 / std::max(a.dhw, 1) + 2;
-    for (const vsrk_tensor5* t : {x, y, mask}) {
-      if (t && 2 * (span_n * t->sn + (int64_t)a.dhw * t->sw + t->c) >= 0x7FFFFFF0ll) return 0;
-    }
-  }
-  static int ablate = -1;
-  if (ablate < 0) {
-    const char* e = getenv("VSRK_PW_ABLATE");
-    ablate = e ? atoi(e) : 0;
-  }
-  a.ablate = ablate;
-  a.cin = x->c;
-  a.cout = y->c;
-  a.ci_pad = cip;
-  a.co_rows = round_up(y->c, 128);
-  a.prologue = d->prologue;
-  a.act = d->act;
-  a.accumulate = d->accumulate;
-  a.has_mask = mask != nullptr;
-  a.out_scale = d->out_scale;
+  if (!pw_fill_args(a, d, x, w_packed, bias, pro_scale, pro_shift, mask, y, cip)) return 0;
   if (a.nvox == 0) return 1;
   const bool pro = d->prologue != VSRK_PRO_NONE;
   if (narrow) {
@@ -1008,6 +1153,81 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
   return 1;
 }
 
+extern "C" size_t vsrk_conv_fwd_reduce_workspace(void) {
+  return (size_t)pw_num_cus() * (PW_THR / 64) * 64 * 16 * sizeof(float);
+}
+
+extern "C" int vsrk_conv_fwd_reduce(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed,
+                                    const float* bias, const float* pro_scale, const float* pro_shift,
+                                    const vsrk_tensor5* y, int32_t mode, const vsrk_tensor5* bnx, const float* scale,
+                                    const float* shift, const float* mean, const float* invstd, float* out_a,
+                                    float* out_b, void* workspace, size_t workspace_bytes, void* stream) {
+  VSRK_CHECK(d && x && y && w_packed && out_a && out_b, "conv_fwd_reduce: null argument");
+  VSRK_CHECK(mode == 1 || mode == 2, "conv_fwd_reduce: mode must be 1 (statistics) or 2 (BN+ReLU backward)");
+  hipStream_t s = (hipStream_t)stream;
+  // eligible: a square pointwise conv on the staged kernel, no epilogue operands
+  if (!pw_enabled() || !vsrk_is16(x->dtype) || y->dtype != x->dtype) return VSRK_ERR_UNSUPPORTED;
+  if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->pd || d->ph || d->pw || d->bias_perm_r > 1) return VSRK_ERR_UNSUPPORTED;
+  if (d->act != VSRK_ACT_NONE || d->accumulate || d->out_scale != 1.f) return VSRK_ERR_UNSUPPORTED;
+  if ((mode == 1) != (d->prologue != VSRK_PRO_NONE)) return VSRK_ERR_UNSUPPORTED;
+  if (x->n != y->n || x->d != y->d || x->h != y->h || x->w != y->w || x->c != y->c) return VSRK_ERR_UNSUPPORTED;
+  if (!dhw_dense(x) || !dhw_dense(y) || !chunk_ok(x, 2) || !chunk_ok(y, 2) || x->c % 32) return VSRK_ERR_UNSUPPORTED;
+  const int ncb = x->c / 32;
+  if (ncb < 2 || ncb > 7) return VSRK_ERR_UNSUPPORTED;
+  if (mode == 2) {
+    VSRK_CHECK(bnx && scale && shift && mean && invstd, "conv_fwd_reduce: mode 2 needs bnx and the BN constants");
+    if (bnx->dtype != x->dtype || bnx->n != y->n || bnx->d != y->d || bnx->h != y->h || bnx->w != y->w ||
+        bnx->c != y->c || !dhw_dense(bnx) || !chunk_ok(bnx, 2))
+      return VSRK_ERR_UNSUPPORTED;
+  }
+  PwArgs a;
+  if (!pw_fill_args(a, d, x, w_packed, bias, pro_scale, pro_shift, nullptr, y, x->c)) return VSRK_ERR_UNSUPPORTED;
+  if (mode == 2) {
+    const int64_t span_n = 32 * 4 / std::max(a.dhw, 1) + 2;
+    if (2 * (span_n * bnx->sn + (int64_t)a.dhw * bnx->sw + bnx->c) >= 0x7FFFFFF0ll) return VSRK_ERR_UNSUPPORTED;
+    a.bnx = bnx->ptr;
+    a.bsn = bnx->sn;
+    a.bsw = bnx->sw;
+    a.bsc = scale;
+    a.bsh = shift;
+    a.bmu = mean;
+    a.bis = invstd;
+  }
+  VSRK_CHECK(workspace && workspace_bytes >= vsrk_conv_fwd_reduce_workspace(),
+             "conv_fwd_reduce: workspace %zu < %zu bytes", workspace_bytes, vsrk_conv_fwd_reduce_workspace());
+  a.red_ws = (float*)workspace;
+  if (a.nvox == 0) {
+    (void)hipMemsetAsync(out_a, 0, sizeof(float) * y->c, s);
+    (void)hipMemsetAsync(out_b, 0, sizeof(float) * y->c, s);
+    return VSRK_OK;
+  }
+  int grid = 0;
+  vsrk_dispatch16(x->dtype, [&](auto tag) {
+    using H = decltype(tag);
+    auto go = [&](auto ncb_c) {
+      constexpr int NC = decltype(ncb_c)::value;
+      a.ntiles = ceil_div(a.nvox, 32 * pw_m<NC>());
+      grid = std::min(pw_grid(a.ntiles), pw_num_cus());
+      if (mode == 1) launch_fwd_reduce<NC, pw_m<NC>(), 1, H>(a, grid, s);
+      else launch_fwd_reduce<NC, pw_m<NC>(), 2, H>(a, grid, s);
+    };
+    switch (ncb) {
+      case 2: go(std::integral_constant<int, 2>{}); break;
+      case 3: go(std::integral_constant<int, 3>{}); break;
+      case 4: go(std::integral_constant<int, 4>{}); break;
+      case 5: go(std::integral_constant<int, 5>{}); break;
+      case 6: go(std::integral_constant<int, 6>{}); break;
+      default: go(std::integral_constant<int, 7>{}); break;
+    }
+    return 0;
+  });
+  VSRK_LAUNCH_CHECK("conv_fwd_reduce");
+  const int ocpr = ncb * 4;
+  pw_red_final_kernel<<<y->c, 256, 0, s>>>(a.red_ws, grid, 32 * ncb, ocpr, 64 / ocpr, y->c, out_a, out_b);
+  VSRK_LAUNCH_CHECK("conv_fwd_reduce_final");
+  return VSRK_OK;
+}
+
 namespace {
 struct PwWPlan {
   bool ok;
@@ -1028,8 +1248,19 @@ PwWPlan pw_wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk
   const int cob = ceil_div(dy->c, 32), cib = ceil_div(x->c, 32);
   p.nco = std::min(cob, 8);
   p.co_chunks = ceil_div(cob, p.nco);
-  p.ncit = std::min(cib, 8);
+  // input chunks of <= 4 blocks, balanced (5 -> 3 + 2): one block per wave
+  // and a stage small enough for two workgroups per CU.  Up to 8 blocks per
+  // chunk (VSRK_PW_WGRAD_CI8=1: waves own blocks w and w + 4) read dY once
+  // but ran 2.3-2.5 TB/s at 160-224 channels (one workgroup per CU, wave 0
+  // holding two blocks of five) against 4.4-4.8 TB/s at <= 128.
+  static int ci8 = -1;
+  if (ci8 < 0) {
+    const char* e = getenv("VSRK_PW_WGRAD_CI8");
+    ci8 = (e && e[0] == '1') ? 1 : 0;
+  }
+  p.ncit = std::min(cib, ci8 ? 8 : 4);
   p.ci_chunks = ceil_div(cib, p.ncit);
+  if (!ci8) p.ncit = ceil_div(cib, p.ci_chunks);
   if (p.nco < 2) return p;
   p.ncoiw = ceil_div(p.ncit, 4);
   p.nchunks = p.co_chunks * p.ci_chunks;

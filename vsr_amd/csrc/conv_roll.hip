@@ -76,7 +76,10 @@ struct RollGeo {
 
 // Epilogue forms (compile time): out = fma(acc, out_scale, bias*out_scale)
 // [relu | prelu] [* (mask > 0)] [+ residual] [+ out]
-enum { RE_RES = 1, RE_MASK = 2, RE_ACC = 4, RE_RELU = 8, RE_PRELU = 16 };
+// RE_PMASK: the PReLU backward of the output's consumer fused in (mask = the
+// PReLU's forward output at y's element offsets; * a where it is <= 0) with
+// per-lane partials of the slope gradient (drf_net.py:56-106 PReLUs)
+enum { RE_RES = 1, RE_MASK = 2, RE_ACC = 4, RE_RELU = 8, RE_PRELU = 16, RE_PMASK = 32 };
 // sub-pixel operand (2-D forms): none, input view, output view
 enum { SP_NONE = 0, SP_X = 1, SP_Y = 2 };
 constexpr int RMAXSUB = 64;  // chunk / block table entries (1024 logical channels)
@@ -117,6 +120,9 @@ struct RollArgs {
   // the element offset of its channels inside the shuffled operand (phase
   // row / column + physical channel) and its tap mask (bit kh*3 + kw)
   const float* act_param;
+  int prio;  // A/B knob (VSRK_ROLL_PRIO=1): s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD)
+  const float* mask_slope;  // RE_PMASK: the PReLU slope a (device scalar)
+  float* slope_ws;          // RE_PMASK: [block][wave][lane] partials
   int spoff[RMAXSUB];
   uint16_t sptap[RMAXSUB];
 };
@@ -140,6 +146,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   float* lbias = reinterpret_cast<float*>(lds + RNSLOT * RSLOT);  // [cout_pad] bias * out_scale
   float* lsc = lbias + a.cout_pad;                                // [cin_pad] prologue scale / shift
   float* lsh = lsc + a.cin_pad;
@@ -420,6 +427,8 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // 4 channels (8 bytes) per lane and channel group.
   const float osc = a.out_scale;
   const float pslope = (EM & RE_PRELU) ? *a.act_param : 0.f;
+  const float mslope = (EM & RE_PMASK) ? *a.mask_slope : 0.f;
+  float sacc = 0.f;  // RE_PMASK: this lane's sum_{mask < 0} out * mask
   auto epilogue = [&](const f32x16 (&A)[RMS], const RTile& tl, int dz, int nt, bool use_pre)
                       __attribute__((always_inline)) {
 #pragma unroll
@@ -530,6 +539,19 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) t[e] = m[e] > 0.f ? t[e] : 0.f;
           }
+          if constexpr (EM & RE_PMASK) {
+            const uint4 mv = *reinterpret_cast<const uint4*>(reinterpret_cast<const H*>(a.msk.ptr) +
+                                                             (yp - reinterpret_cast<H*>(a.y.ptr)));
+            float m[8];
+            Chunk<H>::unpack(mv, m);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) t[e] = m[e] > 0.f ? t[e] : mslope * t[e];
+            float tr[8];
+            Chunk<H>::unpack(Chunk<H>::pack(t), tr);  // the stored (rounded) values, as prelu_bwd reads them
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (m[e] < 0.f) sacc = fmaf(tr[e], m[e], sacc);
+          }
           if constexpr (EM & RE_RES) {
             uint4 rv;
             if constexpr (PREF) {
@@ -590,7 +612,10 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   };
   // compute walk: tile ct (decoded when the walk enters it), slice cs, chunk cc
   int t = t_lo + jb;
-  if (t >= t_hi) return;
+  if (t >= t_hi) {
+    if constexpr (EM & RE_PMASK) a.slope_ws[(blockIdx.x * RNW + wave) * 64 + lane] = 0.f;
+    return;
+  }
   Walk nx;
   nx.t = t;
   nx.sl = 0;
@@ -721,6 +746,29 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   roll_wait_vmcnt<0>();  // the last stage's prefetch
   if (ppre) settle();
   flush(ptl, pdi, true, ppre, fscr);
+  if constexpr (EM & RE_PMASK) a.slope_ws[(blockIdx.x * RNW + wave) * 64 + lane] = sacc;
+}
+
+// da [+]= (sum of the partials, fixed order, double) / a^2: the PReLU slope
+// gradient sum_{y<0} dx * y / a^2 as prelu_bwd_kernel + prelu_final_kernel
+// (drf.hip) compute it
+__global__ __launch_bounds__(256) void roll_slope_final_kernel(const float* __restrict__ part, int n,
+                                                               const float* __restrict__ a, float* __restrict__ da,
+                                                               int accumulate) {
+  __shared__ double sh[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) sh[threadIdx.x] += sh[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double av = (double)*a;
+    const float v = (float)(sh[0] / (av * av));
+    *da = accumulate ? *da + v : v;
+  }
 }
 
 int g_roll_mode = -1;  // -1: from VSRK_CONV_ROLL (default on), 0 off, 1 on
@@ -759,9 +807,12 @@ extern "C" int vsrk_conv_set_roll_depth(int32_t depths) {
 void vsrk_conv_set_roll_mode(int mode) { g_roll_mode = mode; }
 
 // 1 = launched, 0 = not eligible, < 0 = -(error status)
+size_t vsrk_roll_slope_ws_floats() { return (size_t)roll_num_cus() * RNW * 64; }
+
 int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
-                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s) {
+                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s, float* slope_ws,
+                       int* slope_blocks) {
   if (g_roll_mode < 0) {
     const char* e = getenv("VSRK_CONV_ROLL");
     g_roll_mode = (e && e[0] == '0') ? 0 : 1;
@@ -773,7 +824,16 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   // depth-1 slices with 64-channel output blocks (cout a multiple of 64)
   const bool k3 = d->kd == 3;
   if (!k3 && !(d->kd == 1 && d->pd == 0 && y->c % 64 == 0)) return 0;
-  if (d->bias_perm_r > 1 || d->mask_slope) return 0;
+  // PReLU-backward mask (slope_ws): the mask has y's geometry and strides
+  const bool pmask = slope_ws != nullptr;
+  if (d->bias_perm_r > 1 || (d->mask_slope && !pmask)) return 0;
+  if (pmask) {
+    if (!mask || !d->mask_slope || residual || d->kd != 1 || d->prologue) return 0;
+    if (mask->dtype != y->dtype || mask->shuffle != y->shuffle || mask->n != y->n || mask->d != y->d ||
+        mask->h != y->h || mask->w != y->w || mask->c != y->c || mask->sn != y->sn || mask->sd != y->sd ||
+        mask->sh != y->sh || mask->sw != y->sw)
+      return 0;
+  }
   if (d->act == VSRK_ACT_PRELU && (k3 || !d->act_param)) return 0;
   if (k3 && (residual || mask || d->accumulate)) return 0;
   // sub-pixel operands (2-D only, one of x / y): each 16-channel input chunk
@@ -836,6 +896,14 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   a.out_scale = d->out_scale;
   a.nchunk = x->c / RCH;
   a.act_param = d->act_param;
+  {
+    static int prio = -1;
+    if (prio < 0) {
+      const char* e = getenv("VSRK_ROLL_PRIO");
+      prio = (e && e[0] == '1') ? 1 : 0;
+    }
+    a.prio = prio;
+  }
   if (sp != SP_NONE) {
     const vsrk_tensor5* t = sp == SP_X ? x : y;
     const int r = t->shuffle, cph = t->c / (r * r), step = sp == SP_X ? RCH : 32;
@@ -877,8 +945,11 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   if (lds > 160 * 1024) return 0;
   const int grid = (int)vsrk_capped_grid(std::min<int64_t>(ntiles, roll_num_cus()));
   const bool relu = d->act == VSRK_ACT_RELU;
-  const int em = (residual ? RE_RES : 0) | (mask ? RE_MASK : 0) | (d->accumulate ? RE_ACC : 0) | (relu ? RE_RELU : 0) |
-                 (d->act == VSRK_ACT_PRELU ? RE_PRELU : 0);
+  const int em = (residual ? RE_RES : 0) | (mask ? (pmask ? RE_PMASK : RE_MASK) : 0) | (d->accumulate ? RE_ACC : 0) |
+                 (relu ? RE_RELU : 0) | (d->act == VSRK_ACT_PRELU ? RE_PRELU : 0);
+  a.mask_slope = d->mask_slope;
+  a.slope_ws = slope_ws;
+  if (slope_blocks) *slope_blocks = grid;
   int rc = vsrk_dispatch16(x->dtype, [&](auto tag) {
     using H = decltype(tag);
     if (k3) {
@@ -886,15 +957,19 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
       return relu ? launch_roll<3, 1, 0, RE_RELU, SP_NONE, H>(a, lds, grid, s) : launch_roll<3, 1, 0, 0, SP_NONE, H>(a, lds, grid, s);
     }
     // 2-D forms of the EDSR body and its backward: plain, ReLU, residual,
-    // ReLU mask, residual + accumulate (with or without the BN prologue: none
-    // of EDSR's convs has one, the generic path serves it); DRF's sub-pixel
+    // ReLU mask, residual + accumulate; DUF's tail conv (1,3,3) 256 -> 256
+    // with the BN+ReLU prologue (duf_net.py:116-118); DRF's sub-pixel
     // projections: plain, PReLU, accumulate over a shuffled input or output
-    if (d->prologue) return (int)VSRK_ERR_UNSUPPORTED;
+    if (d->prologue) {
+      if (sp != SP_NONE || em != 0) return (int)VSRK_ERR_UNSUPPORTED;
+      return launch_roll<1, 2, 1, 0, SP_NONE, H>(a, lds, grid, s);
+    }
     if (sp == SP_X) {
       switch (em) {
         case 0: return launch_roll<1, 2, 0, 0, SP_X, H>(a, lds, grid, s);
         case RE_PRELU: return launch_roll<1, 2, 0, RE_PRELU, SP_X, H>(a, lds, grid, s);
         case RE_ACC: return launch_roll<1, 2, 0, RE_ACC, SP_X, H>(a, lds, grid, s);
+        case RE_PMASK: return launch_roll<1, 2, 0, RE_PMASK, SP_X, H>(a, lds, grid, s);
         default: return (int)VSRK_ERR_UNSUPPORTED;
       }
     }
@@ -903,6 +978,7 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
         case 0: return launch_roll<1, 2, 0, 0, SP_Y, H>(a, lds, grid, s);
         case RE_PRELU: return launch_roll<1, 2, 0, RE_PRELU, SP_Y, H>(a, lds, grid, s);
         case RE_ACC: return launch_roll<1, 2, 0, RE_ACC, SP_Y, H>(a, lds, grid, s);
+        case RE_PMASK: return launch_roll<1, 2, 0, RE_PMASK, SP_Y, H>(a, lds, grid, s);
         default: return (int)VSRK_ERR_UNSUPPORTED;
       }
     }
@@ -917,4 +993,23 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   });
   if (rc == VSRK_ERR_UNSUPPORTED) return 0;
   return rc == VSRK_OK ? 1 : -rc;
+}
+
+extern "C" size_t vsrk_conv_prelu_bwd_workspace(void) { return vsrk_roll_slope_ws_floats() * sizeof(float); }
+
+extern "C" int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed,
+                                       const float* bias, const vsrk_tensor5* y_fwd, const vsrk_tensor5* y, float* da,
+                                       int32_t accumulate_da, void* workspace, size_t workspace_bytes, void* stream) {
+  VSRK_CHECK(d && x && y && y_fwd && w_packed && da && d->mask_slope, "conv_fwd_prelu_bwd: null argument");
+  VSRK_CHECK(workspace && workspace_bytes >= vsrk_conv_prelu_bwd_workspace(),
+             "conv_fwd_prelu_bwd: workspace %zu < %zu bytes", workspace_bytes, vsrk_conv_prelu_bwd_workspace());
+  hipStream_t s = (hipStream_t)stream;
+  int nb = 0;
+  const int rc = vsrk_conv_fwd_roll(d, x, w_packed, bias, nullptr, nullptr, nullptr, y_fwd, y, s, (float*)workspace, &nb);
+  if (rc == 0) return VSRK_ERR_UNSUPPORTED;
+  if (rc < 0) return -rc;
+  roll_slope_final_kernel<<<1, 256, 0, s>>>((const float*)workspace, nb * RNW * 64, d->mask_slope, da,
+                                            accumulate_da);
+  VSRK_LAUNCH_CHECK("conv_fwd_prelu_bwd_final");
+  return VSRK_OK;
 }

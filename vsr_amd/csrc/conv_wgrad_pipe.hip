@@ -95,8 +95,14 @@ struct WpGeom {
   static constexpr int NCH = MAXY + MAXX;      // chunks per thread per tile
   static constexpr int XSSTEP = GTHR / XCPV;   // slot stride between a thread's X chunks
   static constexpr int SLOTP = MAXX * XSSTEP;  // padded slots: every chunk role has a home (no branch)
-  static constexpr int YBYTES = NCO * VOX * PB;
-  static constexpr int STAGE = YBYTES + NCI * SLOTP * PB;
+  // channel-block planes padded by 64 B: the two planes an 8-lane group of a
+  // commit's ds_write_b128 touches (lanes 0-3 block 0, 4-7 block 1) would
+  // otherwise start on the same bank (plane sizes are multiples of 256 B):
+  // 26 % of LDS cycles were bank conflicts (PMC, EDSR 64->64 wgrad)
+  static constexpr int YPL = VOX * PB + 64;
+  static constexpr int XPL = SLOTP * PB + 64;
+  static constexpr int YBYTES = NCO * YPL;
+  static constexpr int STAGE = YBYTES + NCI * XPL;
   static size_t lds_bytes() {
     const size_t red = NV > 1 ? (size_t)NCO * NCI * TAPS * 1024 * sizeof(float) : 0;
     const size_t bias = (size_t)GTHR * 8 * sizeof(float);
@@ -137,8 +143,8 @@ __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) vo
   const int yc = co0 + (yrem >> 2) * 32 + (yrem & 3) * 8;
   const int xc = ci0 + (xrem >> 2) * 32 + (xrem & 3) * 8;
   const bool yc_ok = yc < a.cout, xc_ok = xc < a.cin;
-  const int ydst = (yrem >> 2) * VOX * PB + (yrem & 3) * 16;
-  const int xdst = (xrem >> 2) * SLOTP * PB + (xrem & 3) * 16;
+  const int ydst = (yrem >> 2) * G::YPL + (yrem & 3) * 16;
+  const int xdst = (xrem >> 2) * G::XPL + (xrem & 3) * 16;
   const int ybase_vox = tid / YCPV, xbase_slot = tid / XCPV;
   constexpr int YVSTEP = GTHR / YCPV, XSSTEP = G::XSSTEP;
   // byte offsets within an (n, d) slice, relative to the tile origin.  A
@@ -337,8 +343,8 @@ __global__ __attribute__((amdgpu_waves_per_eu(1, 1))) __launch_bounds__(GTHR) vo
     advance(c2);
     const bool have_nn = c2.t < t_end;
     const TileRefs rnn = tile_refs(have_nn ? c2 : cfirst);
-    const char* py = cur + cos_ * VOX * PB;
-    const char* px = cur + YBYTES + cis * SLOTP * PB;
+    const char* py = cur + cos_ * G::YPL;
+    const char* px = cur + YBYTES + cis * G::XPL;
     // Row-reuse walk: a wave holds the dY fragments of its ROWS rows (both
     // 16-voxel halves) and walks the XR = ROWS + 2 input rows once; each
     // input fragment (row xr, half c, tap kw) serves every kh with dY row

@@ -74,6 +74,7 @@ struct WRArgs {
   int cin, cout, prologue, want_bias;
   int dzc, ntiles, tps, nsplit, nci_chunks, nco_tiles, slab, kd_bias;
   RDivW tiles_w, tiles_h, nzc;
+  int prio;  // A/B knob (VSRK_ROLL_PRIO=1): s_setprio 1 for waves 4-7
 };
 
 __device__ __attribute__((aligned(256))) uint4 g_wroll_zero[16];
@@ -111,6 +112,7 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   const int coh = wave & 1, cih = (wave >> 1) & 1, vh = wave >> 2;  // output half, input half, row half
 
   // ---- which (channel block, split) this workgroup is ----
@@ -527,6 +529,14 @@ int vsrk_conv_wgrad_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const v
   a.nco_tiles = dy->c / 32;
   a.slab = 9 * 1024 + 32;
   a.kd_bias = std::min(d->pd, 2);
+  {
+    static int prio = -1;
+    if (prio < 0) {
+      const char* e = getenv("VSRK_ROLL_PRIO");
+      prio = (e && e[0] == '1') ? 1 : 0;
+    }
+    a.prio = prio;
+  }
   a.tiles_w = make_rdivw(ceil_div(dy->w, TW));
   a.tiles_h = make_rdivw(ceil_div(dy->h, WTH));
   a.nzc = make_rdivw(ceil_div(dy->d, dzc));

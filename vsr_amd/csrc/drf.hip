@@ -93,7 +93,7 @@ __global__ void subpixel_fold_kernel(const float* __restrict__ dweq, const float
   }
 }
 
-constexpr int PRELU_BLOCKS = 512;
+constexpr int PRELU_BLOCKS = 2048;  // 8 per CU: enough loads in flight for the high-res rows
 
 template <typename T>
 __global__ __launch_bounds__(256) void prelu_partial_kernel(View y, View dx, int64_t nvox, double* __restrict__ part) {
@@ -239,6 +239,51 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(View y, View dy, View dy
       const T* gr = reinterpret_cast<const T*>(dy.ptr) + roff(dy, r) + c0;
       const T* g2r = has2 ? reinterpret_cast<const T*>(dy2.ptr) + roff(dy2, r) + c0 : gr;
       T* orow = reinterpret_cast<T*>(dx.ptr) + roff(dx, r) + c0;
+      if (vfull) {
+        // U voxels per pass with every load issued first (up to 3U 16-byte
+        // loads in flight per thread; one at a time streamed the high-res
+        // gradients at ~2.5 TB/s); same voxel order for the slope partial
+        constexpr int U = 4;
+        for (int wb = vl; wb < y.w; wb += U * vpb) {
+          uint4 ry[U], rg[U], rg2[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int w = wb + u * vpb;
+            ry[u] = rg[u] = rg2[u] = make_uint4(0, 0, 0, 0);
+            if (w < y.w) {
+              ry[u] = *reinterpret_cast<const uint4*>(yr + (int64_t)w * y.sw);
+              rg[u] = *reinterpret_cast<const uint4*>(gr + (int64_t)w * dy.sw);
+              if (has2) rg2[u] = *reinterpret_cast<const uint4*>(g2r + (int64_t)w * dy2.sw);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int w = wb + u * vpb;
+            if (w >= y.w) break;
+            float yv[E], g[E], o[E];
+            Chunk<T>::unpack(ry[u], yv);
+            Chunk<T>::unpack(rg[u], g);
+            if (has2) {
+              float g2[E];
+              Chunk<T>::unpack(rg2[u], g2);
+#pragma unroll
+              for (int e = 0; e < E; ++e) g[e] += g2[e];
+            }
+#pragma unroll
+            for (int e = 0; e < E; ++e) o[e] = yv[e] > 0.f ? g[e] : av * g[e];
+            const uint4 ov = Chunk<T>::pack(o);
+            *reinterpret_cast<uint4*>(orow + (int64_t)w * dx.sw) = ov;
+            float orr[E];
+            Chunk<T>::unpack(ov, orr);  // the rounded stored value, as in the reference's dtype
+            float acc = 0.f;
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+              if (yv[e] < 0.f) acc = fmaf(orr[e], yv[e], acc);
+            s += acc;
+          }
+        }
+        continue;
+      }
       for (int w = vl; w < y.w; w += vpb) {
         const T* py = yr + (int64_t)w * y.sw;
         const T* pg = gr + (int64_t)w * dy.sw;

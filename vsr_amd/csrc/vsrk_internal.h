@@ -23,9 +23,15 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
 
 // rolling-depth 16-bit Conv3d 3x3x3 (conv_roll.hip): forward / data gradient;
 // same return convention; vsrk_conv_set_roll_mode: -1 env VSRK_CONV_ROLL, 0 off, 1 on
+// slope_ws != nullptr (2-D forms): mask is a PReLU output y_fwd with y's
+// geometry and strides, desc->mask_slope its slope a: out = conv * (y_fwd > 0 ?
+// 1 : a) and per-lane partials of sum_{y_fwd < 0} out * y_fwd into slope_ws
+// (vsrk_roll_slope_ws_floats() floats); *slope_blocks = the grid.
 int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
-                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
+                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s, float* slope_ws = nullptr,
+                       int* slope_blocks = nullptr);
+size_t vsrk_roll_slope_ws_floats();
 void vsrk_conv_set_roll_mode(int mode);
 
 // pointwise (1x1x1) bf16 conv (conv_pw.hip): forward / data gradient and

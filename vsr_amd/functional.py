@@ -192,6 +192,55 @@ def conv(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, *, bias: to
     return y
 
 
+def conv_prelu_bwd(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, y_fwd: torch.Tensor,
+                   a: torch.Tensor, da: torch.Tensor, accumulate_da: bool, *, x_shuffle: int = 1, y_shuffle: int = 1,
+                   subpixel: int = 0) -> bool:
+    """y = conv(x) * (y_fwd > 0 ? 1 : a) and da [+]= the PReLU slope gradient
+    (vsrk_conv_fwd_prelu_bwd): conv followed by prelu_bwd(y_fwd, y, a, y, da)
+    in one kernel.  False when the shape is not eligible (nothing launched)."""
+    lib = _lib()
+    d = _desc(k, pad, mask_slope=a, subpixel=subpixel)
+    xv, yv, mv = N.t5(x, x_shuffle), N.t5(y, y_shuffle), N.t5(y_fwd, y_shuffle)
+    ws = workspace(lib.vsrk_conv_prelu_bwd_workspace(), y.device)
+    rc = lib.vsrk_conv_fwd_prelu_bwd(C.byref(d), C.byref(xv), wp.data_ptr(), None, C.byref(mv), C.byref(yv),
+                                     da.data_ptr(), 1 if accumulate_da else 0, ws.data_ptr(), ws.numel(),
+                                     N.stream_ptr(y.device))
+    if rc == 2:  # VSRK_ERR_UNSUPPORTED
+        return False
+    N.check(rc, "conv_fwd_prelu_bwd")
+    return True
+
+
+def conv_reduce(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, *, bias: torch.Tensor | None = None,
+                prologue: int = PRO_NONE, pro_scale: torch.Tensor | None = None,
+                pro_shift: torch.Tensor | None = None, bnx: torch.Tensor | None = None,
+                st: torch.Tensor | None = None) -> torch.Tensor | None:
+    """A 1x1x1 conv into y with a per-channel reduction of y fused into its
+    store pass (vsrk_conv_fwd_reduce): with a prologue (bnx None) the
+    (sum, sumsq) statistics of y, as bn_stats(y); without, given the BN
+    input bnx and its bn_finalize constants st, (sum dy', sum dy' xhat) of
+    the BN+ReLU backward with dz = y, as bn_relu_bwd_reduce(bnx, y, st).
+    -> (2, C) fp32, or None when the shape is not eligible (nothing was
+    launched: the caller runs conv + the separate reduction)."""
+    lib = _lib()
+    mode = 2 if bnx is not None else 1
+    d = _desc((1, 1, 1), (0, 0, 0), prologue)
+    c = y.shape[-1]
+    out = torch.empty((2, c), dtype=torch.float32, device=y.device)
+    ws = workspace(lib.vsrk_conv_fwd_reduce_workspace(), y.device)
+    xv, yv = N.t5(x), N.t5(y)
+    bv = N.t5(bnx) if bnx is not None else None
+    rc = lib.vsrk_conv_fwd_reduce(C.byref(d), C.byref(xv), wp.data_ptr(), N.ptr(bias), N.ptr(pro_scale),
+                                  N.ptr(pro_shift), C.byref(yv), mode, C.byref(bv) if bv is not None else None,
+                                  *(st[i].data_ptr() if st is not None else None for i in range(4)),
+                                  out[0].data_ptr(), out[1].data_ptr(), ws.data_ptr(), ws.numel(),
+                                  N.stream_ptr(y.device))
+    if rc == 2:  # VSRK_ERR_UNSUPPORTED
+        return None
+    N.check(rc, "conv_fwd_reduce")
+    return out
+
+
 def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, k, pad, dw: torch.Tensor, dbias: torch.Tensor | None = None, *,
                prologue: int = PRO_NONE, pro_scale: torch.Tensor | None = None,
                pro_shift: torch.Tensor | None = None, dy_scale: float = 1.0, perm_r: int = 1,

@@ -271,9 +271,6 @@ class _DRFBase(BaseNet):
         def new(hh, ww, c):
             return torch.empty((b, 1, hh, ww, c), dtype=cd, device=dev)
 
-        def zeros(hh, ww, c):
-            return torch.zeros((b, 1, hh, ww, c), dtype=cd, device=dev)
-
         def gbuf(prm):
             key = id(prm)
             if key in bufs:
@@ -334,9 +331,16 @@ class _DRFBase(BaseNet):
             # f_block out: f_features feeds the skip and the next frame's hidden state
             gout = prelu(rc["ffeat"], gfeat, fb.out_block.prelu, new(h, w, f), dy2=d_hidden)
             wgrad(fb.out_block.conv, L[..., f:], gout, K1, P0)
-            dL = zeros(h, w, (G + 1) * f)
-            dHc = zeros(H, W, G * f)
-            F.conv(gout, pw(fb.out_block.conv, 1), dL[..., f:], K1, P0, accumulate=True)
+            # Concat gradients without zero fills (the high-res one is 0.5 GB
+            # per frame at cfg 3): the first contributor to a slice writes it,
+            # later ones accumulate.  dL[..., f:] is first written by the
+            # out_block's data gradient; dHc (every slice) by the last group's
+            # 1x1 down-projection gradient (group 0's strided conv when G = 1);
+            # dL[..., :f] has mixed first contributors and is zeroed.
+            dL = new(h, w, (G + 1) * f)
+            dL[..., :f].zero_()
+            dHc = new(H, W, G * f)
+            F.conv(gout, pw(fb.out_block.conv, 1), dL[..., f:], K1, P0)
             for i in range(G - 1, -1, -1):
                 up, dn = fb.up_blocks[i], fb.down_blocks[i]
                 # down projection -> lr_{i+1} = L[..., (i+1)f:(i+2)f]
@@ -348,12 +352,16 @@ class _DRFBase(BaseNet):
                 wq1, _ = sp(cv, False, 1)
                 spc = F.subpixel_code(k, s, p, False, True)
                 if i == 0:
-                    F.conv(gl, wq1, dHc[..., :f], K3, P1, y_shuffle=s, accumulate=True, subpixel=spc)
+                    F.conv(gl, wq1, dHc[..., :f], K3, P1, y_shuffle=s, accumulate=G > 1, subpixel=spc)
                 else:
-                    dt2 = F.conv(gl, wq1, new(H, W, f), K3, P1, y_shuffle=s, subpixel=spc)
-                    prelu(rc["t2s"][i], dt2, dn.prelu1, dt2)
+                    dt2 = new(H, W, f)
+                    da, acc = gbuf(dn.prelu1.weight)
+                    if not F.conv_prelu_bwd(gl, wq1, dt2, K3, P1, rc["t2s"][i], dn.prelu1.weight, da, acc,
+                                            y_shuffle=s, subpixel=spc):
+                        F.conv(gl, wq1, dt2, K3, P1, y_shuffle=s, subpixel=spc)
+                        F.prelu_bwd(rc["t2s"][i], dt2, dn.prelu1.weight, dt2, da, acc)
                     wgrad(dn.conv1, Hc[..., :(i + 1) * f], dt2, K1, P0)
-                    F.conv(dt2, pw(dn.conv1, 1), dHc[..., :(i + 1) * f], K1, P0, accumulate=True)
+                    F.conv(dt2, pw(dn.conv1, 1), dHc[..., :(i + 1) * f], K1, P0, accumulate=i != G - 1)
                 # up projection -> hr_i = Hc[..., i f:(i+1) f]
                 dec, dpr = (up.deconv, up.prelu) if i == 0 else (up.deconv2, up.prelu2)
                 sh = slice(i * f, (i + 1) * f)
@@ -365,8 +373,12 @@ class _DRFBase(BaseNet):
                 if i == 0:
                     F.conv(gh, wq1, dL[..., :f], K3, P1, x_shuffle=s, accumulate=True, subpixel=spc)
                 else:
-                    dt1 = F.conv(gh, wq1, new(h, w, f), K3, P1, x_shuffle=s, subpixel=spc)
-                    prelu(rc["t1s"][i], dt1, up.prelu1, dt1)
+                    dt1 = new(h, w, f)
+                    da, acc = gbuf(up.prelu1.weight)
+                    if not F.conv_prelu_bwd(gh, wq1, dt1, K3, P1, rc["t1s"][i], up.prelu1.weight, da, acc,
+                                            x_shuffle=s, subpixel=spc):
+                        F.conv(gh, wq1, dt1, K3, P1, x_shuffle=s, subpixel=spc)
+                        F.prelu_bwd(rc["t1s"][i], dt1, up.prelu1.weight, dt1, da, acc)
                     wgrad(up.conv1, L[..., :(i + 1) * f], dt1, K1, P0)
                     F.conv(dt1, pw(up.conv1, 1), dL[..., :(i + 1) * f], K1, P0, accumulate=True)
             g0 = prelu(L[..., :f], dL[..., :f], fb.in_block.prelu, new(h, w, f))

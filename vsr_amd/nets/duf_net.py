@@ -118,13 +118,15 @@ class DUFNet(BaseNet):
         st.count = count
         return st
 
-    def _bn_backward_reduce(self, bn, x, dz, st, grads):
+    def _bn_backward_reduce(self, bn, x, dz, st, grads, red=None):
         """The reduce half of the BN+ReLU backward: writes dgamma / dbeta and
         returns (the (sum_dy, sum_dy_xhat) that feed the input gradient, the
         work handle of their SyncBN all-reduce or None).  The all-reduce is
         asynchronous: the caller queues independent work (a weight gradient)
-        before waiting on the handle."""
-        red = F.bn_relu_bwd_reduce(x, dz, st)
+        before waiting on the handle.  red: the sums when the producing conv
+        already reduced them (F.conv_reduce)."""
+        if red is None:
+            red = F.bn_relu_bwd_reduce(x, dz, st)
         # dgamma / dbeta are this rank's local sums: the data-parallel gradient
         # average (GradSync) combines them across ranks, as torch's
         # SyncBatchNorm does.  Only the copy that feeds the input gradient is
@@ -182,9 +184,14 @@ class DUFNet(BaseNet):
             R = C[:, lo:hi, :, :, :f]
             st1 = self._bn_forward(u.bn1, R, window_sums(lo, hi, f))
             t1 = torch.empty((n, hi - lo, h, w, f), dtype=cd, device=dev)
-            F.conv(R, F.pack_weight(u.conv1.weight, 0, cd), t1, (1, 1, 1), (0, 0, 0), bias=u.conv1.bias,
-                   prologue=ARF, pro_scale=st1[0], pro_shift=st1[1])
-            st2 = self._bn_forward(u.bn2, t1)
+            w1 = F.pack_weight(u.conv1.weight, 0, cd)
+            # bn2's statistics come out of conv1's store pass (no second read of t1)
+            sums2 = F.conv_reduce(R, w1, t1, bias=u.conv1.bias, prologue=ARF, pro_scale=st1[0],
+                                  pro_shift=st1[1]) if self.training else None
+            if sums2 is None:
+                F.conv(R, w1, t1, (1, 1, 1), (0, 0, 0), bias=u.conv1.bias, prologue=ARF, pro_scale=st1[0],
+                       pro_shift=st1[1])
+            st2 = self._bn_forward(u.bn2, t1, sums2)
             olo, ohi = (lo, hi) if keep else (lo + 1, hi - 1)
             pad = (1, 1, 1) if keep else (0, 1, 1)
             F.conv(t1, F.pack_weight(u.conv2.weight, 0, cd), C[:, olo:ohi, :, :, f:f + g], (3, 3, 3), pad,
@@ -298,8 +305,13 @@ class DUFNet(BaseNet):
                 work2.wait()
             dt1 = torch.empty_like(t1)
             F.bn_relu_bwd_apply(t1, dz2, st2, u.bn2.weight, red2, st2.count, dt1, False)
-            dz1 = dgrad(u.conv1, dt1, dz2, K1, P0)  # dz2 is dead: reuse its storage
-            red1, work1 = self._bn_backward_reduce(u.bn1, R, dz1, st1, grads)
+            # dz2 is dead: dz1 reuses its storage; bn1's backward reduce comes
+            # out of the data gradient's store pass where the shape allows
+            dz1 = dz2
+            pre1 = F.conv_reduce(dt1, F.pack_weight(u.conv1.weight, 1, cd), dz1, bnx=R, st=st1)
+            if pre1 is None:
+                dgrad(u.conv1, dt1, dz1, K1, P0)
+            red1, work1 = self._bn_backward_reduce(u.bn1, R, dz1, st1, grads, red=pre1)
             works.append(work1)
             wgrad(u.conv1, R, dt1, K1, P0, prologue=ARF, pro_scale=st1[0], pro_shift=st1[1])
             pending.append((lo, hi, f, dz1, st1, u.bn1.weight, red1, st1.count))
