@@ -121,11 +121,14 @@ int vsrk_conv_fwd(const vsrk_conv_desc* desc, const vsrk_tensor5* x, const void*
  *          scale + shift > 0) and xhat = (bnx - mean) * invstd, out_a =
  *          sum dy', out_b = sum dy' * xhat -- vsrk_bn_relu_bwd_reduce of bn1
  *          without a second pass over y.
- * Square convs (cin = cout, 64..224 channels), no activation / mask /
- * residual / accumulate; VSRK_ERR_UNSUPPORTED otherwise (the caller runs
- * vsrk_conv_fwd + the separate reduction).  Fixed-order partials
- * (deterministic); workspace vsrk_conv_fwd_reduce_workspace() bytes. */
-size_t vsrk_conv_fwd_reduce_workspace(void);
+ * Square pointwise convs (cin = cout, 64..224 channels), no activation /
+ * mask / residual / accumulate; and, mode 2 only, the data gradient of a
+ * Conv3d 3x3x3 on the rolling kernel (a dense unit's conv2 feeding bn2's
+ * backward, duf_net.py:198-203; bnx with y's geometry and strides).
+ * VSRK_ERR_UNSUPPORTED otherwise (the caller runs vsrk_conv_fwd + the separate
+ * reduction).  Fixed-order partials (deterministic); workspace
+ * vsrk_conv_fwd_reduce_workspace(desc, y) bytes. */
+size_t vsrk_conv_fwd_reduce_workspace(const vsrk_conv_desc* desc, const vsrk_tensor5* y);
 int vsrk_conv_fwd_reduce(const vsrk_conv_desc* desc, const vsrk_tensor5* x, const void* w_packed,
                          const float* bias, const float* pro_scale, const float* pro_shift,
                          const vsrk_tensor5* y, int32_t mode, const vsrk_tensor5* bnx, const float* scale,

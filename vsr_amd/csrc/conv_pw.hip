@@ -1153,8 +1153,10 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
   return 1;
 }
 
-extern "C" size_t vsrk_conv_fwd_reduce_workspace(void) {
-  return (size_t)pw_num_cus() * (PW_THR / 64) * 64 * 16 * sizeof(float);
+extern "C" size_t vsrk_conv_fwd_reduce_workspace(const vsrk_conv_desc* d, const vsrk_tensor5* y) {
+  const size_t pw = (size_t)pw_num_cus() * (PW_THR / 64) * 64 * 16 * sizeof(float);
+  if (d && y && d->kd == 3) return std::max(pw, vsrk_roll_bnred_ws_floats(y) * sizeof(float));
+  return pw;
 }
 
 extern "C" int vsrk_conv_fwd_reduce(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed,
@@ -1165,6 +1167,23 @@ extern "C" int vsrk_conv_fwd_reduce(const vsrk_conv_desc* d, const vsrk_tensor5*
   VSRK_CHECK(d && x && y && w_packed && out_a && out_b, "conv_fwd_reduce: null argument");
   VSRK_CHECK(mode == 1 || mode == 2, "conv_fwd_reduce: mode must be 1 (statistics) or 2 (BN+ReLU backward)");
   hipStream_t s = (hipStream_t)stream;
+  if (mode == 2 && d->kd == 3) {
+    // the data gradient of a dense unit's Conv3d 3x3x3 (conv2) feeding bn2's
+    // backward: the rolling kernel's epilogue form (conv_roll.hip)
+    VSRK_CHECK(bnx && scale && shift && mean && invstd, "conv_fwd_reduce: mode 2 needs bnx and the BN constants");
+    VSRK_CHECK(workspace, "conv_fwd_reduce: null workspace");
+    vsrk_roll_bnred r{bnx, scale, shift, mean, invstd, (float*)workspace, workspace_bytes / sizeof(float), 0, 0};
+    const int rc = vsrk_conv_fwd_roll(d, x, w_packed, bias, nullptr, nullptr, nullptr, nullptr, y, s, nullptr,
+                                      nullptr, &r);
+    if (rc == 0) return VSRK_ERR_UNSUPPORTED;
+    if (rc < 0) return -rc;
+    if (r.ntiles == 0) {
+      (void)hipMemsetAsync(out_a, 0, sizeof(float) * y->c, s);
+      (void)hipMemsetAsync(out_b, 0, sizeof(float) * y->c, s);
+      return VSRK_OK;
+    }
+    return vsrk_roll_bnred_final(r, y->c, out_a, out_b, s);
+  }
   // eligible: a square pointwise conv on the staged kernel, no epilogue operands
   if (!pw_enabled() || !vsrk_is16(x->dtype) || y->dtype != x->dtype) return VSRK_ERR_UNSUPPORTED;
   if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->pd || d->ph || d->pw || d->bias_perm_r > 1) return VSRK_ERR_UNSUPPORTED;
@@ -1193,8 +1212,8 @@ extern "C" int vsrk_conv_fwd_reduce(const vsrk_conv_desc* d, const vsrk_tensor5*
     a.bmu = mean;
     a.bis = invstd;
   }
-  VSRK_CHECK(workspace && workspace_bytes >= vsrk_conv_fwd_reduce_workspace(),
-             "conv_fwd_reduce: workspace %zu < %zu bytes", workspace_bytes, vsrk_conv_fwd_reduce_workspace());
+  VSRK_CHECK(workspace && workspace_bytes >= vsrk_conv_fwd_reduce_workspace(d, y),
+             "conv_fwd_reduce: workspace %zu < %zu bytes", workspace_bytes, vsrk_conv_fwd_reduce_workspace(d, y));
   a.red_ws = (float*)workspace;
   if (a.nvox == 0) {
     (void)hipMemsetAsync(out_a, 0, sizeof(float) * y->c, s);

@@ -79,7 +79,11 @@ struct RollGeo {
 // RE_PMASK: the PReLU backward of the output's consumer fused in (mask = the
 // PReLU's forward output at y's element offsets; * a where it is <= 0) with
 // per-lane partials of the slope gradient (drf_net.py:56-106 PReLUs)
-enum { RE_RES = 1, RE_MASK = 2, RE_ACC = 4, RE_RELU = 8, RE_PRELU = 16, RE_PMASK = 32 };
+// RE_BNRED (3-D form): the reduce half of the BN+ReLU backward whose dz this
+// data gradient is (duf_net.py:198-203: bn2 before conv2) fused into the
+// epilogue: per tile and wave, (sum dy', sum dy' xhat) of its 32 channels
+// with dy' = out * (bnx * scale + shift > 0), xhat = (bnx - mean) * invstd
+enum { RE_RES = 1, RE_MASK = 2, RE_ACC = 4, RE_RELU = 8, RE_PRELU = 16, RE_PMASK = 32, RE_BNRED = 64 };
 // sub-pixel operand (2-D forms): none, input view, output view
 enum { SP_NONE = 0, SP_X = 1, SP_Y = 2 };
 constexpr int RMAXSUB = 64;  // chunk / block table entries (1024 logical channels)
@@ -123,6 +127,11 @@ struct RollArgs {
   int prio;  // A/B knob (VSRK_ROLL_PRIO=1): s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD)
   const float* mask_slope;  // RE_PMASK: the PReLU slope a (device scalar)
   float* slope_ws;          // RE_PMASK: [block][wave][lane] partials
+  // RE_BNRED: the BN input (y's geometry and strides), its per-channel
+  // constants and the [tile][wave][2 halves][16 sum + 16 sum-xhat] slab
+  const char* bnx;
+  const float *bn_sc, *bn_sh, *bn_mu, *bn_is;
+  float* red_ws;
   int spoff[RMAXSUB];
   uint16_t sptap[RMAXSUB];
 };
@@ -152,6 +161,20 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   float* lsh = lsc + a.cin_pad;
   if constexpr (PRO) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, a.cin_pad, tid, RNW * 64);
   for (int i = tid; i < a.cout_pad; i += RNW * 64) lbias[i] = (a.bias && i < a.cout) ? a.bias[i] * a.out_scale : 0.f;
+  // RE_BNRED: [4][cout_pad] BN constants after the prologue tables
+  float* lbn = lbias + a.cout_pad + 2 * a.cin_pad;
+  if constexpr ((EM & RE_BNRED) != 0) {
+    for (int i = tid; i < a.cout_pad; i += RNW * 64) {
+      const bool ok = i < a.cout;
+      lbn[i] = ok ? a.bn_sc[i] : 0.f;
+      lbn[a.cout_pad + i] = ok ? a.bn_sh[i] : 0.f;
+      lbn[2 * a.cout_pad + i] = ok ? a.bn_mu[i] : 0.f;
+      lbn[3 * a.cout_pad + i] = ok ? a.bn_is[i] : 0.f;
+    }
+  }
+  float rs1[(EM & RE_BNRED) ? 16 : 1], rs2[(EM & RE_BNRED) ? 16 : 1];  // this lane's 16 channels
+#pragma unroll
+  for (int i = 0; i < ((EM & RE_BNRED) ? 16 : 1); ++i) rs1[i] = rs2[i] = 0.f;
 
   // ---- per-lane DMA roles, fixed for the launch ----
   // piece j = wave + RNW*q fills slot bytes [j KB, j+1 KB); lane l writes 16
@@ -205,12 +228,14 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // A tile as the walks need it.  Order: output-channel tile fastest (they
   // share the input), then the depth run, columns, rows, sample.
   struct RTile {
+    int t;  // tile index
     int h0, w0, n0, z0, z1, di_lo, nsl, nb;
     int xo;  // element offset of halo origin (nb, di = 0, h0 - ph, w0 - pw) in x
     int yo;  // element offset of (nb, dz = 0, h0, w0, n0) in y
   };
   auto decode = [&](int t) __attribute__((always_inline)) {
     RTile tl;
+    tl.t = t;
     int u = rdiv(t, a.ntn);
     tl.n0 = (t - u * (int)a.ntn.d) * 32 * NT;
     int v = rdiv(u, a.nzc);
@@ -470,6 +495,24 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
 #pragma unroll
               for (int e = 0; e < 4; ++e) v[e] += rr[e];
             }
+            if constexpr (EM & RE_BNRED) {
+              float vr[4], xb[4];
+              unpack_pk<H>(pack_pk<H, uint2>(v), vr);  // the stored (rounded) dz, as the separate reduce reads it
+              unpack_pk<H>(*reinterpret_cast<const uint2*>(reinterpret_cast<const H*>(a.bnx) +
+                                                          (yp - reinterpret_cast<H*>(a.y.ptr)) + 8 * g), xb);
+              const float4 c_sc = *reinterpret_cast<const float4*>(lbn + co);
+              const float4 c_sh = *reinterpret_cast<const float4*>(lbn + a.cout_pad + co);
+              const float4 c_mu = *reinterpret_cast<const float4*>(lbn + 2 * a.cout_pad + co);
+              const float4 c_is = *reinterpret_cast<const float4*>(lbn + 3 * a.cout_pad + co);
+              const float csc[4] = {c_sc.x, c_sc.y, c_sc.z, c_sc.w}, csh[4] = {c_sh.x, c_sh.y, c_sh.z, c_sh.w};
+              const float cmu[4] = {c_mu.x, c_mu.y, c_mu.z, c_mu.w}, cis[4] = {c_is.x, c_is.y, c_is.z, c_is.w};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float dy = fmaf(xb[e], csc[e], csh[e]) > 0.f ? vr[e] : 0.f;
+                rs1[4 * g + e] += dy;
+                rs2[4 * g + e] = fmaf(dy, (xb[e] - cmu[e]) * cis[e], rs2[4 * g + e]);
+              }
+            }
             if constexpr (EM & RE_ACC) {
               float o[4];
               unpack_pk<H>(*reinterpret_cast<const uint2*>(yp + 8 * g), o);
@@ -597,6 +640,30 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
           for (int m = 0; m < RMS; ++m)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[b][m][i] = 0.f;
+        }
+      }
+      if constexpr ((EM & RE_BNRED) != 0) {
+        if (all) {
+          // the tile's partials: butterfly over the 32 voxel lanes of each
+          // half (fixed order), lane 0 / 32 writes its half's 16 channels
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+#pragma unroll
+            for (int off = 1; off < 32; off <<= 1) {
+              rs1[i] += __shfl_xor(rs1[i], off);
+              rs2[i] += __shfl_xor(rs2[i], off);
+            }
+          }
+          if (r == 0) {
+            float* o = a.red_ws + ((int64_t)tl.t * RNW + wave) * 64 + hf * 32;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              o[i] = rs1[i];
+              o[16 + i] = rs2[i];
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < 16; ++i) rs1[i] = rs2[i] = 0.f;
         }
       }
     } else {
@@ -749,6 +816,40 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   if constexpr (EM & RE_PMASK) a.slope_ws[(blockIdx.x * RNW + wave) * 64 + lane] = sacc;
 }
 
+// Channel c of the fused BN+ReLU backward reduce: the (tile, wave) partials
+// of the tiles whose output block holds c (tile order: block fastest), in a
+// fixed order, in double.  c = n0 + 8g + 4hf + e -> half hf, index 4g + e.
+__global__ __launch_bounds__(256) void roll_bnred_final_kernel(const float* __restrict__ ws, int ntiles, int ntn,
+                                                               int cout, float* __restrict__ o1,
+                                                               float* __restrict__ o2) {
+  const int c = blockIdx.x;
+  if (c >= cout) return;
+  const int blk = c >> 5, cc = c & 31, hfc = (cc >> 2) & 1, idx = 4 * (cc >> 3) + (cc & 3);
+  const int nt = (ntiles - blk + ntn - 1) / ntn;  // tiles blk, blk + ntn, ...
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = threadIdx.x; i < nt * RNW; i += 256) {
+    const int t = blk + ntn * (i / RNW), w = i % RNW;
+    const float* p = ws + ((int64_t)t * RNW + w) * 64 + hfc * 32;
+    s1 += p[idx];
+    s2 += p[16 + idx];
+  }
+  __shared__ double r1[256], r2[256];
+  r1[threadIdx.x] = s1;
+  r2[threadIdx.x] = s2;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) {
+      r1[threadIdx.x] += r1[threadIdx.x + k];
+      r2[threadIdx.x] += r2[threadIdx.x + k];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    o1[c] = (float)r1[0];
+    o2[c] = (float)r2[0];
+  }
+}
+
 // da [+]= (sum of the partials, fixed order, double) / a^2: the PReLU slope
 // gradient sum_{y<0} dx * y / a^2 as prelu_bwd_kernel + prelu_final_kernel
 // (drf.hip) compute it
@@ -812,7 +913,7 @@ size_t vsrk_roll_slope_ws_floats() { return (size_t)roll_num_cus() * RNW * 64; }
 int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                        const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s, float* slope_ws,
-                       int* slope_blocks) {
+                       int* slope_blocks, vsrk_roll_bnred* bnred) {
   if (g_roll_mode < 0) {
     const char* e = getenv("VSRK_CONV_ROLL");
     g_roll_mode = (e && e[0] == '0') ? 0 : 1;
@@ -836,12 +937,19 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   }
   if (d->act == VSRK_ACT_PRELU && (k3 || !d->act_param)) return 0;
   if (k3 && (residual || mask || d->accumulate)) return 0;
+  if (bnred) {
+    const vsrk_tensor5* b = bnred->bnx;
+    if (!k3 || d->prologue || d->act != VSRK_ACT_NONE || !b || b->dtype != y->dtype || b->shuffle > 1 ||
+        b->n != y->n || b->d != y->d || b->h != y->h || b->w != y->w || b->c != y->c || b->sn != y->sn ||
+        b->sd != y->sd || b->sh != y->sh || b->sw != y->sw)
+      return 0;
+  }
   // sub-pixel operands (2-D only, one of x / y): each 16-channel input chunk
   // (x) or 32-channel output block (y) must lie inside one phase
   const int sp = x->shuffle > 1 ? SP_X : (y->shuffle > 1 ? SP_Y : SP_NONE);
   if (x->shuffle > 1 && y->shuffle > 1) return 0;
   if (sp != SP_NONE) {
-    if (k3 || d->prologue || residual || mask) return 0;
+    if (k3 || d->prologue || residual || (mask && !pmask)) return 0;
     const vsrk_tensor5* t = sp == SP_X ? x : y;
     const int r = t->shuffle, cph = t->c / (r * r);
     if (cph * r * r != t->c || cph % (sp == SP_X ? RCH : 32) != 0) return 0;
@@ -857,7 +965,7 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
            t->sw % 4 == 0;
   };
   if (y->c % 4 != 0 || !out_ok(y)) return 0;
-  if ((residual && !out_ok(residual)) || (mask && !out_ok(mask))) return 0;
+  if ((residual && !out_ok(residual)) || (mask && !pmask && !out_ok(mask))) return 0;
   for (const vsrk_tensor5* t : {x, y, residual, mask}) {  // every element offset fits in 32 bits
     if (!t) continue;
     const int64_t r = t->shuffle > 1 ? t->shuffle : 1;
@@ -941,7 +1049,19 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   VSRK_CHECK(ntiles < (1ll << 31), "conv_fwd(roll): too many tiles");
   a.ntiles = (int)ntiles;
   const size_t slot = k3 ? RollGeo<3, 1>::SLOT : RollGeo<1, 2>::SLOT;
-  const size_t lds = (size_t)RNSLOT * slot + (size_t)a.cout_pad * 4 + (d->prologue ? 2 * (size_t)a.cin_pad * 4 : 0);
+  const size_t lds = (size_t)RNSLOT * slot + (size_t)a.cout_pad * 4 +
+                     (d->prologue || bnred ? 2 * (size_t)a.cin_pad * 4 : 0) + (bnred ? 4 * (size_t)a.cout_pad * 4 : 0);
+  if (bnred) {
+    if (bnred->ws_floats < (size_t)ntiles * RNW * 64) return 0;
+    a.bnx = (const char*)bnred->bnx->ptr;
+    a.bn_sc = bnred->scale;
+    a.bn_sh = bnred->shift;
+    a.bn_mu = bnred->mean;
+    a.bn_is = bnred->invstd;
+    a.red_ws = bnred->ws;
+    bnred->ntiles = (int)ntiles;
+    bnred->ntn = ntn;
+  }
   if (lds > 160 * 1024) return 0;
   const int grid = (int)vsrk_capped_grid(std::min<int64_t>(ntiles, roll_num_cus()));
   const bool relu = d->act == VSRK_ACT_RELU;
@@ -953,6 +1073,7 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   int rc = vsrk_dispatch16(x->dtype, [&](auto tag) {
     using H = decltype(tag);
     if (k3) {
+      if (bnred) return launch_roll<3, 1, 0, RE_BNRED, SP_NONE, H>(a, lds, grid, s);
       if (d->prologue) return relu ? launch_roll<3, 1, 1, RE_RELU, SP_NONE, H>(a, lds, grid, s) : launch_roll<3, 1, 1, 0, SP_NONE, H>(a, lds, grid, s);
       return relu ? launch_roll<3, 1, 0, RE_RELU, SP_NONE, H>(a, lds, grid, s) : launch_roll<3, 1, 0, 0, SP_NONE, H>(a, lds, grid, s);
     }
@@ -988,6 +1109,7 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
       case RE_RES: return launch_roll<1, 2, 0, RE_RES, SP_NONE, H>(a, lds, grid, s);
       case RE_MASK: return launch_roll<1, 2, 0, RE_MASK, SP_NONE, H>(a, lds, grid, s);
       case RE_RES | RE_ACC: return launch_roll<1, 2, 0, RE_RES | RE_ACC, SP_NONE, H>(a, lds, grid, s);
+      case RE_PMASK: return launch_roll<1, 2, 0, RE_PMASK, SP_NONE, H>(a, lds, grid, s);
       default: return (int)VSRK_ERR_UNSUPPORTED;
     }
   });
@@ -1012,4 +1134,14 @@ extern "C" int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* d, const vsrk_tenso
                                             accumulate_da);
   VSRK_LAUNCH_CHECK("conv_fwd_prelu_bwd_final");
   return VSRK_OK;
+}
+
+int vsrk_roll_bnred_final(const vsrk_roll_bnred& r, int cout, float* sum_dy, float* sum_dy_xhat, hipStream_t s) {
+  roll_bnred_final_kernel<<<cout, 256, 0, s>>>(r.ws, r.ntiles, r.ntn, cout, sum_dy, sum_dy_xhat);
+  VSRK_LAUNCH_CHECK("conv_fwd_reduce(roll) final");
+  return VSRK_OK;
+}
+
+size_t vsrk_roll_bnred_ws_floats(const vsrk_tensor5* y) {  // every depth its own tile run (an upper bound)
+  return (size_t)y->n * ceil_div(y->h, RFTH) * ceil_div(y->w, TW) * ceil_div(y->c, 32) * std::max(y->d, 1) * RNW * 64;
 }

@@ -27,10 +27,23 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
 // geometry and strides, desc->mask_slope its slope a: out = conv * (y_fwd > 0 ?
 // 1 : a) and per-lane partials of sum_{y_fwd < 0} out * y_fwd into slope_ws
 // (vsrk_roll_slope_ws_floats() floats); *slope_blocks = the grid.
+// bnred (3-D form, no epilogue operands): the fused BN+ReLU backward reduce
+// (bnx with y's geometry and strides; ws >= ntiles * 8 * 64 floats); on
+// launch ntiles / ntn are filled for roll_bnred_final.
+struct vsrk_roll_bnred {
+  const vsrk_tensor5* bnx;
+  const float *scale, *shift, *mean, *invstd;
+  float* ws;
+  size_t ws_floats;
+  int ntiles, ntn;
+};
 int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                        const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s, float* slope_ws = nullptr,
-                       int* slope_blocks = nullptr);
+                       int* slope_blocks = nullptr, vsrk_roll_bnred* bnred = nullptr);
+// the fused reduce's final per-channel sums (roll_bnred_final_kernel)
+int vsrk_roll_bnred_final(const vsrk_roll_bnred& r, int cout, float* sum_dy, float* sum_dy_xhat, hipStream_t s);
+size_t vsrk_roll_bnred_ws_floats(const vsrk_tensor5* y);
 size_t vsrk_roll_slope_ws_floats();
 void vsrk_conv_set_roll_mode(int mode);
 

@@ -214,9 +214,10 @@ def conv_prelu_bwd(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, y
 def conv_reduce(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, *, bias: torch.Tensor | None = None,
                 prologue: int = PRO_NONE, pro_scale: torch.Tensor | None = None,
                 pro_shift: torch.Tensor | None = None, bnx: torch.Tensor | None = None,
-                st: torch.Tensor | None = None) -> torch.Tensor | None:
+                st: torch.Tensor | None = None, k=(1, 1, 1), pad=(0, 0, 0)) -> torch.Tensor | None:
     """A 1x1x1 conv into y with a per-channel reduction of y fused into its
-    store pass (vsrk_conv_fwd_reduce): with a prologue (bnx None) the
+    store pass (vsrk_conv_fwd_reduce; k = (3, 3, 3): the data gradient of a
+    Conv3d 3x3x3 on the rolling kernel, bnx form only): with a prologue (bnx None) the
     (sum, sumsq) statistics of y, as bn_stats(y); without, given the BN
     input bnx and its bn_finalize constants st, (sum dy', sum dy' xhat) of
     the BN+ReLU backward with dz = y, as bn_relu_bwd_reduce(bnx, y, st).
@@ -224,11 +225,11 @@ def conv_reduce(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, *, bias: tor
     launched: the caller runs conv + the separate reduction)."""
     lib = _lib()
     mode = 2 if bnx is not None else 1
-    d = _desc((1, 1, 1), (0, 0, 0), prologue)
+    d = _desc(tuple(k), tuple(pad), prologue)
     c = y.shape[-1]
     out = torch.empty((2, c), dtype=torch.float32, device=y.device)
-    ws = workspace(lib.vsrk_conv_fwd_reduce_workspace(), y.device)
     xv, yv = N.t5(x), N.t5(y)
+    ws = workspace(lib.vsrk_conv_fwd_reduce_workspace(C.byref(d), C.byref(yv)), y.device)
     bv = N.t5(bnx) if bnx is not None else None
     rc = lib.vsrk_conv_fwd_reduce(C.byref(d), C.byref(xv), wp.data_ptr(), N.ptr(bias), N.ptr(pro_scale),
                                   N.ptr(pro_shift), C.byref(yv), mode, C.byref(bv) if bv is not None else None,

@@ -298,8 +298,14 @@ class DUFNet(BaseNet):
             dx_i = dC[:, olo:ohi, :, :, f:f + g]
             # each weight gradient is queued between a BatchNorm reduce and the
             # use of its (SyncBN all-reduced) sums, so it hides the collective
-            dz2 = dgrad(u.conv2, dx_i, torch.empty_like(t1), (3, 3, 3), pad)
-            red2, work2 = self._bn_backward_reduce(u.bn2, t1, dz2, st2, grads)
+            # bn2's backward reduce comes out of conv2's data-gradient epilogue
+            dz2 = torch.empty_like(t1)
+            dpad = tuple(kk - 1 - p for kk, p in zip((3, 3, 3), pad))
+            pre2 = F.conv_reduce(dx_i, F.pack_weight(u.conv2.weight, 1, cd), dz2, bnx=t1, st=st2, k=(3, 3, 3),
+                                 pad=dpad)
+            if pre2 is None:
+                dgrad(u.conv2, dx_i, dz2, (3, 3, 3), pad)
+            red2, work2 = self._bn_backward_reduce(u.bn2, t1, dz2, st2, grads, red=pre2)
             wgrad(u.conv2, t1, dx_i, (3, 3, 3), pad, prologue=ARF, pro_scale=st2[0], pro_shift=st2[1])
             if work2 is not None:
                 work2.wait()
