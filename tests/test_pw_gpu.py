@@ -15,6 +15,14 @@ import torch.nn.functional as Fn
 from vsr_amd import functional as F
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _fused_on(monkeypatch):
+    """the fused entry points are tested whatever VSRK_FUSE says for the nets"""
+    monkeypatch.setattr(F, "FUSE", True)
+
+
 DEV = "cuda"
 BF = torch.bfloat16
 

@@ -7,6 +7,8 @@ CPU or PyTorch fallback.
 """
 from __future__ import annotations
 
+import os
+
 import ctypes as C
 
 import torch
@@ -192,12 +194,19 @@ def conv(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, *, bias: to
     return y
 
 
+# A/B knob: VSRK_FUSE=0 makes the fused conv + reduction / PReLU-backward
+# entry points report "not eligible", so the nets run the separate kernels
+FUSE = os.environ.get("VSRK_FUSE", "1") != "0"
+
+
 def conv_prelu_bwd(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, y_fwd: torch.Tensor,
                    a: torch.Tensor, da: torch.Tensor, accumulate_da: bool, *, x_shuffle: int = 1, y_shuffle: int = 1,
                    subpixel: int = 0) -> bool:
     """y = conv(x) * (y_fwd > 0 ? 1 : a) and da [+]= the PReLU slope gradient
     (vsrk_conv_fwd_prelu_bwd): conv followed by prelu_bwd(y_fwd, y, a, y, da)
     in one kernel.  False when the shape is not eligible (nothing launched)."""
+    if not FUSE:
+        return False
     lib = _lib()
     d = _desc(k, pad, mask_slope=a, subpixel=subpixel)
     xv, yv, mv = N.t5(x, x_shuffle), N.t5(y, y_shuffle), N.t5(y_fwd, y_shuffle)
@@ -223,6 +232,8 @@ def conv_reduce(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, *, bias: tor
     the BN+ReLU backward with dz = y, as bn_relu_bwd_reduce(bnx, y, st).
     -> (2, C) fp32, or None when the shape is not eligible (nothing was
     launched: the caller runs conv + the separate reduction)."""
+    if not FUSE:
+        return None
     lib = _lib()
     mode = 2 if bnx is not None else 1
     d = _desc(tuple(k), tuple(pad), prologue)
