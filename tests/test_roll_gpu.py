@@ -61,7 +61,8 @@ CASES = [
 ]
 
 
-def _run(case, dtype, prologue, depth=0, cap=0, seed=0):
+def _run(case, dtype, prologue, depth=0, cap=0, seed=0, roll=1):
+    """roll=1 forces the rolling kernel (the default skips single output depths)"""
     n, d, h, w, ci, co, pdp, off = case
     g = torch.Generator().manual_seed(seed)
     big = torch.randn((n, d, h, w, ci + off + 8), generator=g)
@@ -81,12 +82,14 @@ def _run(case, dtype, prologue, depth=0, cap=0, seed=0):
     kw = dict(prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV)) if prologue else {}
     F.set_roll_depth(depth)
     F.set_grid_cap(cap)
+    F.set_conv_path("roll", roll)
     try:
         F.conv(big.to(DEV, dtype)[..., off:off + ci], F.pack_weight(wt.to(DEV), 0, dtype), y, (3, 3, 3), pad,
                bias=b.to(DEV), **kw)
     finally:
         F.set_roll_depth(0)
         F.set_grid_cap(0)
+        F.set_conv_path("roll", -1)
     torch.cuda.synchronize()
     # the channels outside the output slice are untouched
     assert (ybig[..., :4].float() == 7.0).all() and (ybig[..., 4 + co:].float() == 7.0).all()
@@ -118,11 +121,7 @@ def test_roll_matches_fast_path():
     16-bit rounding at a DUF unit shape (and the switch really changes path)"""
     case = (2, 7, 16, 64, 64, 32, 1, 0)
     y_roll, ref = _run(case, torch.bfloat16, True)
-    F.set_conv_path("roll", 0)
-    try:
-        y_fast, _ = _run(case, torch.bfloat16, True)
-    finally:
-        F.set_conv_path("roll", -1)
+    y_fast, _ = _run(case, torch.bfloat16, True, roll=0)
     tol = _tol(torch.bfloat16, ref)
     assert (y_roll - ref).abs().max().item() <= tol
     assert (y_fast - ref).abs().max().item() <= tol

@@ -61,7 +61,8 @@ def _reference(case, dtype, prologue, big, gy, sc, sh):
     return wr.grad, br.grad
 
 
-def _run(case, dtype, prologue, big, gy, sc, sh, depth=0, cap=0, roll=-1, bias=True):
+def _run(case, dtype, prologue, big, gy, sc, sh, depth=0, cap=0, roll=1, bias=True):
+    """roll=1 forces the rolling kernel (the default skips <= 3 output depths)"""
     n, d, h, w, ci, co, pdp, off = case
     kw = dict(prologue=F.PRO_AFFINE_RELU, pro_scale=sc.to(DEV), pro_shift=sh.to(DEV)) if prologue else {}
     dw = torch.empty((co, ci, 3, 3, 3), dtype=torch.float32, device=DEV)

@@ -853,15 +853,31 @@ __global__ __launch_bounds__(256) void roll_bnred_final_kernel(const float* __re
 // da [+]= (sum of the partials, fixed order, double) / a^2: the PReLU slope
 // gradient sum_{y<0} dx * y / a^2 as prelu_bwd_kernel + prelu_final_kernel
 // (drf.hip) compute it
-__global__ __launch_bounds__(256) void roll_slope_final_kernel(const float* __restrict__ part, int n,
-                                                               const float* __restrict__ a, float* __restrict__ da,
-                                                               int accumulate) {
-  __shared__ double sh[256];
+// n is a multiple of 4 (RNW * 64 partials per block). One workgroup of 1024
+// lanes, eight independent 16-byte loads in flight per lane before the adds:
+// the partials are latency-bound, not bandwidth-bound (a 256-lane serial loop
+// over 64 K floats ran ~100 us).
+__global__ __launch_bounds__(1024) void roll_slope_final_kernel(const float* __restrict__ part, int n,
+                                                                const float* __restrict__ a, float* __restrict__ da,
+                                                                int accumulate) {
+  constexpr int U = 8;
+  __shared__ double sh[1024];
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  const int n4 = n >> 2;
   double s = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  for (int base = threadIdx.x; base < n4; base += 1024 * U) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * 1024;
+      v[u] = i < n4 ? p4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += ((double)v[u].x + (double)v[u].y) + ((double)v[u].z + (double)v[u].w);
+  }
   sh[threadIdx.x] = s;
   __syncthreads();
-  for (int k = 128; k > 0; k >>= 1) {
+  for (int k = 512; k > 0; k >>= 1) {
     if (threadIdx.x < k) sh[threadIdx.x] += sh[threadIdx.x + k];
     __syncthreads();
   }
@@ -872,7 +888,7 @@ __global__ __launch_bounds__(256) void roll_slope_final_kernel(const float* __re
   }
 }
 
-int g_roll_mode = -1;  // -1: from VSRK_CONV_ROLL (default on), 0 off, 1 on
+int g_roll_mode = -1;  // -1: from VSRK_CONV_ROLL (unset: 2), 0 off, 1 forced on, 2 automatic
 
 int roll_num_cus() {
   static int n = 0;
@@ -916,7 +932,7 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
                        int* slope_blocks, vsrk_roll_bnred* bnred) {
   if (g_roll_mode < 0) {
     const char* e = getenv("VSRK_CONV_ROLL");
-    g_roll_mode = (e && e[0] == '0') ? 0 : 1;
+    g_roll_mode = !e ? 2 : (e[0] == '0' ? 0 : 1);
   }
   if (g_roll_mode == 0) return 0;
   if (!vsrk_is16(x->dtype) || y->dtype != x->dtype) return 0;
@@ -937,6 +953,10 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   }
   if (d->act == VSRK_ACT_PRELU && (k3 || !d->act_param)) return 0;
   if (k3 && (residual || mask || d->accumulate)) return 0;
+  // automatic mode: a single output depth has no slice reuse to roll over;
+  // the per-kd-stage kernel is faster there (DUF's last unit, 3 -> 1 slices
+  // at F = 224: 817 vs 943 us, r3p microbench)
+  if (g_roll_mode == 2 && k3 && y->d == 1 && !bnred && vsrk_g_roll_dz == 0) return 0;
   if (bnred) {
     const vsrk_tensor5* b = bnred->bnx;
     if (!k3 || d->prologue || d->act != VSRK_ACT_NONE || !b || b->dtype != y->dtype || b->shuffle > 1 ||
@@ -1125,12 +1145,13 @@ extern "C" int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* d, const vsrk_tenso
   VSRK_CHECK(d && x && y && y_fwd && w_packed && da && d->mask_slope, "conv_fwd_prelu_bwd: null argument");
   VSRK_CHECK(workspace && workspace_bytes >= vsrk_conv_prelu_bwd_workspace(),
              "conv_fwd_prelu_bwd: workspace %zu < %zu bytes", workspace_bytes, vsrk_conv_prelu_bwd_workspace());
+  VSRK_CHECK(((uintptr_t)workspace & 15) == 0, "conv_fwd_prelu_bwd: workspace must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
   int nb = 0;
   const int rc = vsrk_conv_fwd_roll(d, x, w_packed, bias, nullptr, nullptr, nullptr, y_fwd, y, s, (float*)workspace, &nb);
   if (rc == 0) return VSRK_ERR_UNSUPPORTED;
   if (rc < 0) return -rc;
-  roll_slope_final_kernel<<<1, 256, 0, s>>>((const float*)workspace, nb * RNW * 64, d->mask_slope, da,
+  roll_slope_final_kernel<<<1, 1024, 0, s>>>((const float*)workspace, nb * RNW * 64, d->mask_slope, da,
                                             accumulate_da);
   VSRK_LAUNCH_CHECK("conv_fwd_prelu_bwd_final");
   return VSRK_OK;

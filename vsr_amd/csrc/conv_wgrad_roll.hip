@@ -428,7 +428,7 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
   }
 }
 
-int g_wroll_mode = -1;  // -1: VSRK_WGRAD_ROLL (default on), 0 off, 1 on
+int g_wroll_mode = -1;  // -1: VSRK_WGRAD_ROLL (unset: 2), 0 off, 1 forced on, 2 automatic
 
 int wroll_num_cus() {
   static int n = 0;
@@ -451,9 +451,13 @@ bool vsrk_wgrad_roll_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const 
                           int* tps, int* ntiles, int* dzc, size_t* ws_bytes) {
   if (g_wroll_mode < 0) {
     const char* e = getenv("VSRK_WGRAD_ROLL");
-    g_wroll_mode = (e && e[0] == '0') ? 0 : 1;
+    g_wroll_mode = !e ? 2 : (e[0] == '0' ? 0 : 1);
   }
   if (g_wroll_mode == 0) return false;
+  // automatic mode: with <= 3 output depths the kd-tap reuse of the rolling
+  // walk does not pay for its ring (DUF units 4 / 5: 1619 vs 1764 us and
+  // 755 vs 1159 us for the pipelined kernel, r3p microbench)
+  if (g_wroll_mode == 2 && dy->d <= 3 && vsrk_g_roll_dz == 0) return false;
   if (!vsrk_is16(x->dtype) || dy->dtype != x->dtype) return false;
   if (d->kd != 3 || d->kh != 3 || d->kw != 3 || d->pd < 0 || d->pd > 2 || d->ph < 0 || d->ph > 2 || d->pw < 0 ||
       d->pw > 2)

@@ -22,7 +22,7 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
                        const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
 
 // rolling-depth 16-bit Conv3d 3x3x3 (conv_roll.hip): forward / data gradient;
-// same return convention; vsrk_conv_set_roll_mode: -1 env VSRK_CONV_ROLL, 0 off, 1 on
+// same return convention; vsrk_conv_set_roll_mode: -1 env VSRK_CONV_ROLL, 0 off, 1 forced on, 2 automatic
 // slope_ws != nullptr (2-D forms): mask is a PReLU output y_fwd with y's
 // geometry and strides, desc->mask_slope its slope a: out = conv * (y_fwd > 0 ?
 // 1 : a) and per-lane partials of sum_{y_fwd < 0} out * y_fwd into slope_ws

@@ -277,7 +277,9 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, k, pad, dw: torch.Tensor, dbia
 
 
 def set_conv_path(path: str, mode: int) -> None:
-    """Select a conv kernel family ("fast", "pw", "roll", "thin", "wgrad_pipe", "wgrad_roll"): -1 default, 0 off, 1 on."""
+    """Select a conv kernel family ("fast", "pw", "roll", "thin", "wgrad_pipe", "wgrad_roll"): -1 default, 0 off, 1 on
+    (for "roll" / "wgrad_roll": 1 forces the rolling kernel on every eligible
+    shape, the default also skips shallow output depths where it is slower)."""
     N.check(_lib().vsrk_conv_set_path(path.encode(), int(mode)), "conv_set_path")
 
 
