@@ -18,7 +18,8 @@ from vsr_amd import functional as F  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--what", default="up,down,up_dgrad,down_dgrad,up_wgrad,down_wgrad,hr1x1,hr1x1_dgrad,hr1x1_wgrad")
+    ap.add_argument("--what", default="up,down,up_dgrad,down_dgrad,up_wgrad,down_wgrad,hr1x1,hr1x1_dgrad,hr1x1_wgrad,"
+                                      "prelu_hr,prelu_lr")
     ap.add_argument("--paths", default="")
     args = ap.parse_args()
     _native.load()
@@ -56,6 +57,7 @@ def main():
     dw1 = torch.empty((f, ci1, 1, 1, 1), device=dev)
     db1 = torch.empty(f, device=dev)
     slope = torch.tensor([0.2], device=dev)
+    da = torch.zeros(1, device=dev)
     sub_flop = 2.0 * b * h * w * (s * s * f) * f * 9
     ref_flop = 2.0 * b * H * W * f * f * (k // s) ** 2  # the reference's strided / transposed conv
     pw_flop = 2.0 * b * H * W * ci1 * f
@@ -85,6 +87,11 @@ def main():
         "hr1x1_dgrad": (lambda: F.conv(hr_out, pw1, dHc, K1, P0, accumulate=True), pw_flop,
                         2.0 * b * H * W * (2 * ci1 + f)),
         "hr1x1_wgrad": (lambda: F.conv_wgrad(Hc, hr_out, K1, P0, dw1, db1), pw_flop, 2.0 * b * H * W * (ci1 + f)),
+        # PReLU backward of an up projection's output (a 64-channel slice of the
+        # high-res concat and of its gradient -> a dense buffer) and a low-res one
+        "prelu_hr": (lambda: F.prelu_bwd(Hc[..., f:2 * f], dHc[..., f:2 * f], slope, hr_out, da, True), 0.0,
+                     2.0 * b * H * W * 3 * f),
+        "prelu_lr": (lambda: F.prelu_bwd(lr, lr, slope, out_lr, da, True), 0.0, 2.0 * b * h * w * 3 * f),
     }
     for name in args.what.split(","):
         fn, flop, nbytes = cases[name]
@@ -98,7 +105,7 @@ def main():
         en.record()
         torch.cuda.synchronize()
         ms = st.elapsed_time(en) / args.iters
-        extra = f"  ref-FLOP {ref_flop / ms / 1e9:7.1f} TF/s" if "1x1" not in name else ""
+        extra = f"  ref-FLOP {ref_flop / ms / 1e9:7.1f} TF/s" if "1x1" not in name and flop else ""
         print(f"drf {name:12s} {ms * 1e3:8.1f} us  {flop / ms / 1e9:7.1f} TFLOP/s{extra}  "
               f"{nbytes / ms / 1e9:5.2f} TB/s", flush=True)
 
