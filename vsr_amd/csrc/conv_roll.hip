@@ -117,7 +117,6 @@ struct RollArgs {
   int cin, cout, cin_pad, cout_pad;
   int pd, ph, pw;
   int prologue;
-  int bias_r;  // > 1: bias in torch pixel-shuffle order (a y_shuffle output of perm-packed weights)
   float out_scale;
   int dzc, nchunk, ntiles;
   RDiv ntn, nzc, tiles_w, tiles_h;
@@ -161,19 +160,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   float* lsc = lbias + a.cout_pad;                                // [cin_pad] prologue scale / shift
   float* lsh = lsc + a.cin_pad;
   if constexpr (PRO) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, a.cin_pad, tid, RNW * 64);
-  for (int i = tid; i < a.cout_pad; i += RNW * 64) {
-    float b = 0.f;
-    if (a.bias && i < a.cout) {
-      int cb = i;
-      if (a.bias_r > 1) {  // view order (sub, c') -> torch order c' * r * r + sub
-        const int rr = a.bias_r * a.bias_r, cp = a.cout / rr;
-        const int sub = cb / cp;
-        cb = (cb - sub * cp) * rr + sub;
-      }
-      b = a.bias[cb];
-    }
-    lbias[i] = b * a.out_scale;
-  }
+  for (int i = tid; i < a.cout_pad; i += RNW * 64) lbias[i] = (a.bias && i < a.cout) ? a.bias[i] * a.out_scale : 0.f;
   // RE_BNRED: [4][cout_pad] BN constants after the prologue tables
   float* lbn = lbias + a.cout_pad + 2 * a.cin_pad;
   if constexpr ((EM & RE_BNRED) != 0) {
@@ -840,26 +827,11 @@ __global__ __launch_bounds__(256) void roll_bnred_final_kernel(const float* __re
   const int blk = c >> 5, cc = c & 31, hfc = (cc >> 2) & 1, idx = 4 * (cc >> 3) + (cc & 3);
   const int nt = (ntiles - blk + ntn - 1) / ntn;  // tiles blk, blk + ntn, ...
   double s1 = 0.0, s2 = 0.0;
-  constexpr int U = 8;  // loads in flight per lane before the adds (the partials are latency-bound)
-  const int n = nt * RNW;
-  for (int i0 = threadIdx.x; i0 < n; i0 += 256 * U) {
-    float v1[U], v2[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = i0 + 256 * u;
-      v1[u] = v2[u] = 0.f;
-      if (i < n) {
-        const int t = blk + ntn * (i / RNW), w = i % RNW;
-        const float* p = ws + ((int64_t)t * RNW + w) * 64 + hfc * 32;
-        v1[u] = p[idx];
-        v2[u] = p[16 + idx];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      s1 += v1[u];
-      s2 += v2[u];
-    }
+  for (int i = threadIdx.x; i < nt * RNW; i += 256) {
+    const int t = blk + ntn * (i / RNW), w = i % RNW;
+    const float* p = ws + ((int64_t)t * RNW + w) * 64 + hfc * 32;
+    s1 += p[idx];
+    s2 += p[16 + idx];
   }
   __shared__ double r1[256], r2[256];
   r1[threadIdx.x] = s1;
@@ -971,9 +943,7 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   if (!k3 && !(d->kd == 1 && d->pd == 0 && y->c % 64 == 0)) return 0;
   // PReLU-backward mask (slope_ws): the mask has y's geometry and strides
   const bool pmask = slope_ws != nullptr;
-  if ((d->bias_perm_r > 1 && (y->shuffle != d->bias_perm_r || y->c % (d->bias_perm_r * d->bias_perm_r))) ||
-      (d->mask_slope && !pmask))
-    return 0;
+  if (d->bias_perm_r > 1 || (d->mask_slope && !pmask)) return 0;
   if (pmask) {
     if (!mask || !d->mask_slope || residual || d->kd != 1 || d->prologue) return 0;
     if (mask->dtype != y->dtype || mask->shuffle != y->shuffle || mask->n != y->n || mask->d != y->d ||
@@ -1041,7 +1011,6 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   a.msk = rview(mask ? mask : y);
   a.w = w_packed;
   a.bias = bias;
-  a.bias_r = d->bias_perm_r > 1 ? d->bias_perm_r : 1;
   a.pro_scale = pro_scale;
   a.pro_shift = pro_shift;
   a.cin = x->c;
