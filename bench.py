@@ -273,13 +273,19 @@ def run_model(name, args, world, rank, dev):
     x, y = make_batch(spec["task"], lr, hr)
     l1 = L1Loss()
 
+    def phase(p):
+        if F.timer is not None:
+            F.timer.phase = p
+
     def step():
+        phase("fwd")
         out = net(x)
         if isinstance(out, list):
             loss = torch.stack([l1(o, t) for o, t in zip(out, y)]).mean()
         else:
             loss = l1(out, y)
         opt.zero_grad(set_to_none=True)
+        phase("bwd")
         loss.backward()
         if sync is not None:
             sync.finish()
@@ -327,6 +333,12 @@ def run_model(name, args, world, rank, dev):
     elapsed = time.perf_counter() - t0
     flop, kernel_s, launches = F.timer.totals()
     tsteps = getattr(F.timer, "steps", args.steps)  # steps the kernel timer saw
+    by_dir = {}  # fwd / dgrad / wgrad launches of the roofline kernel on their own
+    for lab in F.timer.labels():
+        f_, t_, n_ = F.timer.totals(lab)
+        by_dir[lab] = {"ms_per_step": t_ / tsteps * 1e3, "launches_per_step": n_ / tsteps,
+                       "tflop_per_step": f_ / tsteps / 1e12,
+                       "frac": (f_ / t_ / PEAK[args.precision]) if t_ > 0 else None}
     F.timer = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
@@ -348,7 +360,7 @@ def run_model(name, args, world, rank, dev):
                      "unit": "TFLOP/s", "frac": achieved / peak if achieved else None, "traffic": traffic,
                      "traffic_kernel": tkern, "kernel": kdesc,
                      "kernel_ms_per_step": kernel_s / tsteps * 1e3, "launches_per_step": launches / tsteps,
-                     "flop_per_step": flop / tsteps},
+                     "flop_per_step": flop / tsteps, "by_direction": by_dir},
         "final_loss": float(loss.item()),
         "graph": graph,
     }
@@ -400,7 +412,9 @@ def worker(args, world, rank, local):
             rf = results["duf"]["roofline"]
             out["north_star"] = {"model": "duf", "kernel": rf["kernel"], "achieved": rf["achieved"],
                                  "peak": rf["peak"], "unit": rf["unit"], "frac": rf["frac"], "target_frac": 0.5,
-                                 "frac_of_measured_peak": rf.get("frac_of_measured_peak")}
+                                 "frac_of_measured_peak": rf.get("frac_of_measured_peak"),
+                                 "launches_per_step": rf["launches_per_step"],
+                                 "tflop_per_step": rf["flop_per_step"] / 1e12, "by_direction": rf["by_direction"]}
         if world == 1 and not args.no_cpu_baseline:
             for m in names:
                 results[m]["cpu_baseline"] = cpu_baseline(m)

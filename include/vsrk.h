@@ -318,6 +318,15 @@ int vsrk_bn_stats_grouped(const vsrk_tensor5* x, int32_t groups, float* sum, flo
 int vsrk_bn_finalize(const float* sum, const float* sumsq, double count, const float* gamma, const float* beta,
                      float eps, float momentum, float* running_mean, float* running_var, float* scale,
                      float* shift, float* mean, float* invstd, int32_t channels, void* stream);
+/* vsrk_bn_finalize with the voxel count read on the device: count =
+ * count_mult * *count_dev (one double).  SyncBatchNorm: count_dev is the
+ * all-reduced N*H*W of the global batch, so no rank reads it on the host
+ * (torch's SyncBatchNorm all-gathers the counts the same way; reference
+ * BatchNorm3d, duf_net.py:116,198,201,209,212). */
+int vsrk_bn_finalize_dcount(const float* sum, const float* sumsq, const double* count_dev, double count_mult,
+                            const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
+                            float* running_var, float* scale, float* shift, float* mean, float* invstd,
+                            int32_t channels, void* stream);
 int vsrk_bn_fold_running(const float* gamma, const float* beta, const float* running_mean,
                          const float* running_var, float eps, float* scale, float* shift, float* mean,
                          float* invstd, int32_t channels, void* stream);

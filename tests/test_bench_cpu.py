@@ -52,3 +52,15 @@ def test_traffic_files_are_per_launch_bytes():
         t, k = bench._traffic(model, "bf16")
         # the forward roofline kernel: the rolling conv (round 3) or the tile kernel
         assert t is None or (t > 1e8 and k.startswith(("conv_roll_kernel", "conv_fast_kernel")))
+
+
+def test_every_conv_entry_point_is_timed():
+    """The north-star roofline counts the fused data gradients too: every conv
+    entry point that can run a roofline kernel launches through timer.wrap
+    (conv_reduce / conv_prelu_bwd were not, so the DUF line
+    counted 12 of its 18 Conv3d 3x3x3 launches)."""
+    import inspect
+
+    from vsr_amd import functional as F
+    for fn in (F.conv, F.conv_reduce, F.conv_prelu_bwd, F.conv_wgrad):
+        assert "timer.wrap(" in inspect.getsource(fn), fn.__name__

@@ -9,6 +9,17 @@ one GPU per rank).
     the samples), local dgamma/dbeta averaged by GradSync.  Also the
     forward outputs and the updated running statistics.
   * DRFNet (BASELINE cfg 3, VSR over frames): per-sample independent.
+  * DUFNet in bf16 with UNEQUAL shards (3 and 1 samples of the 4): the fused
+    BN-reduce paths (16-bit only) feed the async SyncBN all-reduces, and the
+    global voxel count comes from the device-side count all-reduce
+    (SyncBNAllReduce.global_count).  Each rank's mean loss is weighted by
+    its share of the global batch (x world, GradSync averages), so the
+    averaged gradient is the gradient of the global mean.  Same-precision
+    single process as the yardstick: bf16 roundings move with the summation
+    order of the statistics, so gradients rel-L2 <= 3e-2, outputs <= 3e-2.
+  * fp16 overflow on ONE rank (its loss scale forced to 2^40): the inf
+    reaches every rank through the bucket all-reduce and both ranks skip
+    the step (GradSync.finish -> BaseNet.step_ok).
 
 fp32.  The two runs differ only in the summation order of the BatchNorm sums
 and of the weight gradients; DRF is held to 1e-4 rel-L2, DUF to 1e-3 (an
@@ -63,7 +74,17 @@ def _shard(v, rank, world):
     return v[rank * n:(rank + 1) * n]
 
 
-def _worker(rank, world, port, model, q):
+SPLIT = {"equal": None, "uneven": (3, 1)}  # samples per rank (None: batch / world each)
+
+
+def _shard_split(v, rank, split):
+    if isinstance(v, list):
+        return [_shard_split(t, rank, split) for t in v]
+    lo = sum(split[:rank])
+    return v[lo:lo + split[rank]]
+
+
+def _worker(rank, world, port, model, q, precision="fp32", split=None, overflow=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     from vsr_amd.ddp import GradSync, enable_sync_bn
@@ -72,15 +93,25 @@ def _worker(rank, world, port, model, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         net, x, y = _setup(model)
-        net = net.to(dev).set_precision("fp32").train()
+        net = net.to(dev).set_precision(precision).train()
         sync = GradSync(net, world)
         assert enable_sync_bn(net) == (model == "duf")
-        xs = [t.to(dev) for t in _shard(x, rank, world)]
-        ys = _shard(y, rank, world)
+        if split is None:
+            xs, ys = _shard(x, rank, world), _shard(y, rank, world)
+            weight = 1.0
+        else:
+            xs, ys = _shard_split(x, rank, split), _shard_split(y, rank, split)
+            weight = world * split[rank] / sum(split)  # share of the global mean (GradSync averages)
+        xs = [t.to(dev) for t in xs]
         ys = [t.to(dev) for t in ys] if isinstance(ys, list) else ys.to(dev)
+        if overflow:
+            net._scale = 2.0 ** 40 if rank == 0 else 2.0 ** 4
         out = net(xs)
-        _loss(out, ys).backward()
+        (_loss(out, ys) * weight).backward()
         sync.finish()
+        if overflow:
+            q.put((rank, {"step_ok": net.step_ok()}))
+            return
         # numpy arrays travel by value (a shared-memory tensor would outlive its sender)
         outs = [o.detach().cpu().numpy() for o in out] if isinstance(out, list) else out.detach().cpu().numpy()
         res = {"grads": {k: p.grad.detach().cpu().numpy() for k, p in net.named_parameters()},
@@ -91,15 +122,53 @@ def _worker(rank, world, port, model, q):
         dist.destroy_process_group()
 
 
-def _single(model):
+def _single(model, precision="fp32"):
     dev = torch.device("cuda", 0)
     net, x, y = _setup(model)
-    net = net.to(dev).set_precision("fp32").train()
+    net = net.to(dev).set_precision(precision).train()
     out = net([t.to(dev) for t in x])
     _loss(out, [t.to(dev) for t in y] if isinstance(y, list) else y.to(dev)).backward()
     outs = [o.detach().cpu() for o in out] if isinstance(out, list) else out.detach().cpu()
     return {"grads": {k: p.grad.detach().cpu() for k, p in net.named_parameters()}, "out": outs,
             "buffers": {k: v.detach().cpu() for k, v in net.state_dict().items() if "running" in k}}
+
+
+def _run_ranks(model, **kw):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, model, q), kwargs=kw) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=180) for _ in range(2))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    return got
+
+
+def test_fp16_overflow_on_one_rank_skips_on_both():
+    got = _run_ranks("duf", precision="fp16", overflow=True)
+    assert got[0]["step_ok"] is False and got[1]["step_ok"] is False, got
+
+
+def test_duf_bf16_uneven_shards_equal_one_process():
+    ref = _single("duf", "bf16")
+    got = _run_ranks("duf", precision="bf16", split=SPLIT["uneven"])
+    gmax = max(v.norm().item() for v in ref["grads"].values())
+    for rank in (0, 1):
+        g_r = {k: torch.from_numpy(v) for k, v in got[rank]["grads"].items()}
+        for k, g in ref["grads"].items():
+            if g.norm().item() <= 1e-6 * gmax:
+                assert g_r[k].norm().item() <= 1e-2 * gmax, (rank, k)
+                continue
+            rel = (g_r[k] - g).norm().item() / g.norm().item()
+            assert rel <= 3e-2, (rank, k, rel)
+        for k, v in ref["buffers"].items():
+            b = torch.from_numpy(got[rank]["buffers"][k])
+            assert (b - v).abs().max().item() <= 1e-3 * (1 + v.abs().max().item()), k
+        exp = _shard_split(ref["out"], rank, SPLIT["uneven"])
+        assert (torch.from_numpy(got[rank]["out"]) - exp).abs().max().item() <= 3e-2, rank
 
 
 @pytest.mark.parametrize("model", ["duf", "drf"])

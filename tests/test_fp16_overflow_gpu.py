@@ -84,3 +84,22 @@ def test_bf16_has_no_check():
     net.set_precision("bf16")
     assert _step(net, opt, x, y)
     assert net._found_inf is None
+
+
+def test_check_stays_on_at_unit_scale():
+    """The dynamic scale may back off to 1 and below (no floor, as GradScaler):
+    a NaN step at scale 1 is still detected and skipped, and the scale keeps
+    halving (the guard used to switch itself off at scale 1)."""
+    net, opt, x, y = _setup(3)
+    assert _step(net, opt, x, y)
+    net._scale = 1.0
+    before = {k: v.clone() for k, v in net.state_dict().items()}
+    xn = x.clone()
+    xn[0, 0, 3, 5] = float("nan")
+    assert not _step(net, opt, xn, y)
+    assert net._scale == 0.5
+    for k, v in net.state_dict().items():
+        assert torch.equal(v, before[k]), k
+    assert _step(net, opt, x, y)  # finite again at scale 0.5
+    net.loss_scale = 1.0  # a fixed unit scale checks as well
+    assert not _step(net, opt, xn, y)

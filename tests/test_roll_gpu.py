@@ -394,3 +394,34 @@ def test_roll_bn_backward_reduce_fused(case):
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
     err = (outs[0] - ref).abs().max().item()
     assert err <= 1e-5 * (1 + ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("r", [2, 4])
+def test_roll_pixel_shuffle_output_bias(r):
+    """EDSR's upsampler conv (edsr_net.py Upsampler: Conv2d(F, r*r*F, 3) + PixelShuffle(r)):
+    perm-packed weights, a y_shuffle output view and the bias in torch's
+    pixel-shuffle order; the rolling kernel (2-D form, SP_Y) and the tile
+    kernel both match the fp64 conv + pixel shuffle"""
+    g = torch.Generator().manual_seed(11)
+    n, h, w, f = 2, 20, 36, 64
+    co = f * r * r
+    x = torch.randn((n, 1, h, w, f), generator=g)
+    wt = torch.randn((co, f, 3, 3), generator=g) / (9 * f) ** 0.5
+    b = torch.randn(co, generator=g)
+    dt = torch.bfloat16
+    ref = Fn.pixel_shuffle(Fn.conv2d(_q(x, dt)[:, 0].permute(0, 3, 1, 2), _q(wt, dt), b.double(), padding=1), r)
+    ref = ref.permute(0, 2, 3, 1).unsqueeze(1)
+    outs = []
+    for roll in (1, 0):
+        y = torch.full((n, 1, h * r, w * r, f), 7.0, dtype=dt, device=DEV)
+        F.set_conv_path("roll", roll)
+        try:
+            F.conv(x.to(DEV, dt), F.pack_weight(wt.to(DEV), 0, dt, perm_r=r), y, (1, 3, 3), (0, 1, 1),
+                   bias=b.to(DEV), y_shuffle=r)
+        finally:
+            F.set_conv_path("roll", -1)
+        torch.cuda.synchronize()
+        outs.append(y.double().cpu())
+    for y in outs:
+        assert (y - ref).abs().max().item() <= _tol(dt, ref)
+    assert not torch.equal(outs[0], outs[1])  # different accumulation order: the rolling kernel ran

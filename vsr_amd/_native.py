@@ -105,6 +105,8 @@ _SIGS = {
     "vsrk_dcn_coord_grad": (C.c_int, [_P] * 8),
     "vsrk_bn_finalize": (C.c_int, [_P, _P, C.c_double, _P, _P, C.c_float, C.c_float, _P, _P, _P, _P, _P, _P,
                                    C.c_int32, _P]),
+    "vsrk_bn_finalize_dcount": (C.c_int, [_P, _P, _P, C.c_double, _P, _P, C.c_float, C.c_float, _P, _P, _P, _P,
+                                          _P, _P, C.c_int32, _P]),
     "vsrk_bn_fold_running": (C.c_int, [_P, _P, _P, _P, C.c_float, _P, _P, _P, _P, C.c_int32, _P]),
     "vsrk_bn_apply": (C.c_int, [_T5, _P, _P, C.c_int32, _T5, _P]),
     "vsrk_bn_relu_bwd_reduce": (C.c_int, [_T5, _T5, _P, _P, _P, _P, _P, _P, _P, C.c_size_t, _P]),

@@ -174,13 +174,17 @@ __global__ __launch_bounds__(256) void chan_final_kernel(const float* __restrict
   }
 }
 
+// count_dev (may be null): the voxel count is count * *count_dev, read on the
+// device (SyncBN: the global batch's N*H*W, all-reduced without a host read)
 __global__ void bn_finalize_kernel(const float* __restrict__ sum, const float* __restrict__ sumsq, double count,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-                                   float momentum, float* __restrict__ rmean, float* __restrict__ rvar,
-                                   float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ mean,
-                                   float* __restrict__ invstd, int C) {
+                                   const double* __restrict__ count_dev, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float eps, float momentum,
+                                   float* __restrict__ rmean, float* __restrict__ rvar, float* __restrict__ scale,
+                                   float* __restrict__ shift, float* __restrict__ mean, float* __restrict__ invstd,
+                                   int C) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
+  if (count_dev) count *= *count_dev;
   const double m = (double)sum[c] / count;
   double var = (double)sumsq[c] / count - m * m;
   if (var < 0) var = 0;
@@ -544,8 +548,22 @@ extern "C" int vsrk_bn_finalize(const float* sum, const float* sumsq, double cou
                                 int32_t channels, void* stream) {
   VSRK_CHECK(sum && sumsq && scale && shift && mean && invstd && count > 0, "bn_finalize: bad argument");
   bn_finalize_kernel<<<ceil_div(channels, 256), 256, 0, (hipStream_t)stream>>>(
-      sum, sumsq, count, gamma, beta, eps, momentum, running_mean, running_var, scale, shift, mean, invstd, channels);
+      sum, sumsq, count, nullptr, gamma, beta, eps, momentum, running_mean, running_var, scale, shift, mean, invstd,
+      channels);
   VSRK_LAUNCH_CHECK("bn_finalize");
+  return VSRK_OK;
+}
+
+extern "C" int vsrk_bn_finalize_dcount(const float* sum, const float* sumsq, const double* count_dev,
+                                       double count_mult, const float* gamma, const float* beta, float eps,
+                                       float momentum, float* running_mean, float* running_var, float* scale,
+                                       float* shift, float* mean, float* invstd, int32_t channels, void* stream) {
+  VSRK_CHECK(sum && sumsq && count_dev && scale && shift && mean && invstd && count_mult > 0,
+             "bn_finalize_dcount: bad argument");
+  bn_finalize_kernel<<<ceil_div(channels, 256), 256, 0, (hipStream_t)stream>>>(
+      sum, sumsq, count_mult, count_dev, gamma, beta, eps, momentum, running_mean, running_var, scale, shift, mean,
+      invstd, channels);
+  VSRK_LAUNCH_CHECK("bn_finalize_dcount");
   return VSRK_OK;
 }
 

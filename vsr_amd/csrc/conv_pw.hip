@@ -647,11 +647,25 @@ __global__ __launch_bounds__(256) void pw_red_final_kernel(const float* __restri
   const int nlane = rstep;            // lanes of column col: col + ocpr * k, k < rstep
   const int nitems = nbx * (PW_THR / 64) * nlane;
   double s1 = 0.0, s2 = 0.0;
-  for (int i = threadIdx.x; i < nitems; i += 256) {
-    const int k = i % nlane, bw = i / nlane;  // bw = block * waves + wave
-    const float* p = ws + (((int64_t)yc * nbx * (PW_THR / 64) + bw) * 64 + col + ocpr * k) * 16;
-    s1 += p[e];
-    s2 += p[8 + e];
+  constexpr int U = 8;  // loads in flight per lane before the adds (the partials are latency-bound)
+  for (int i0 = threadIdx.x; i0 < nitems; i0 += 256 * U) {
+    float v1[U], v2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + 256 * u;
+      v1[u] = v2[u] = 0.f;
+      if (i < nitems) {
+        const int k = i % nlane, bw = i / nlane;  // bw = block * waves + wave
+        const float* p = ws + (((int64_t)yc * nbx * (PW_THR / 64) + bw) * 64 + col + ocpr * k) * 16;
+        v1[u] = p[e];
+        v2[u] = p[8 + e];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      s1 += v1[u];
+      s2 += v2[u];
+    }
   }
   __shared__ double r1[256], r2[256];
   r1[threadIdx.x] = s1;

@@ -117,6 +117,7 @@ struct RollArgs {
   int cin, cout, cin_pad, cout_pad;
   int pd, ph, pw;
   int prologue;
+  int bias_r;  // > 1: bias in torch pixel-shuffle order (a y_shuffle output of perm-packed weights)
   float out_scale;
   int dzc, nchunk, ntiles;
   RDiv ntn, nzc, tiles_w, tiles_h;
@@ -160,7 +161,19 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   float* lsc = lbias + a.cout_pad;                                // [cin_pad] prologue scale / shift
   float* lsh = lsc + a.cin_pad;
   if constexpr (PRO) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, a.cin_pad, tid, RNW * 64);
-  for (int i = tid; i < a.cout_pad; i += RNW * 64) lbias[i] = (a.bias && i < a.cout) ? a.bias[i] * a.out_scale : 0.f;
+  for (int i = tid; i < a.cout_pad; i += RNW * 64) {
+    float b = 0.f;
+    if (a.bias && i < a.cout) {
+      int cb = i;
+      if (a.bias_r > 1) {  // view order (sub, c') -> torch order c' * r * r + sub
+        const int rr = a.bias_r * a.bias_r, cp = a.cout / rr;
+        const int sub = cb / cp;
+        cb = (cb - sub * cp) * rr + sub;
+      }
+      b = a.bias[cb];
+    }
+    lbias[i] = b * a.out_scale;
+  }
   // RE_BNRED: [4][cout_pad] BN constants after the prologue tables
   float* lbn = lbias + a.cout_pad + 2 * a.cin_pad;
   if constexpr ((EM & RE_BNRED) != 0) {
@@ -172,9 +185,12 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       lbn[3 * a.cout_pad + i] = ok ? a.bn_is[i] : 0.f;
     }
   }
-  float rs1[(EM & RE_BNRED) ? 16 : 1], rs2[(EM & RE_BNRED) ? 16 : 1];  // this lane's 16 channels
+  // RE_BNRED: this lane's partials of its 8-channel column (lane & 3) of the
+  // transposed epilogue
+  constexpr int NRS = (EM & RE_BNRED) ? 8 : 1;
+  float rs1[NRS], rs2[NRS];
 #pragma unroll
-  for (int i = 0; i < ((EM & RE_BNRED) ? 16 : 1); ++i) rs1[i] = rs2[i] = 0.f;
+  for (int i = 0; i < NRS; ++i) rs1[i] = rs2[i] = 0.f;
 
   // ---- per-lane DMA roles, fixed for the launch ----
   // piece j = wave + RNW*q fills slot bytes [j KB, j+1 KB); lane l writes 16
@@ -448,89 +464,18 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     }
   };
 
-  // Epilogue of one finished output depth dz of a tile, output block nt:
-  // 4 channels (8 bytes) per lane and channel group.
   const float osc = a.out_scale;
   const float pslope = (EM & RE_PRELU) ? *a.act_param : 0.f;
   const float mslope = (EM & RE_PMASK) ? *a.mask_slope : 0.f;
   float sacc = 0.f;  // RE_PMASK: this lane's sum_{mask < 0} out * mask
-  auto epilogue = [&](const f32x16 (&A)[RMS], const RTile& tl, int dz, int nt, bool use_pre)
-                      __attribute__((always_inline)) {
-#pragma unroll
-    for (int ms = 0; ms < RMS; ++ms) {
-      const int ho = tl.h0 + wave * RMS + ms, wo = tl.w0 + r;
-      if (ho < a.y.h && wo < a.y.w) {
-        H* yp = reinterpret_cast<H*>(a.y.ptr) +
-                (tl.yo + dz * a.y.sd + (wave * RMS + ms) * a.y.sh + r * a.y.sw + nt * 32 + 4 * hf);
-        const H* rp = nullptr;
-        const H* mp = nullptr;
-        if constexpr (EM & RE_RES)
-          rp = reinterpret_cast<const H*>(a.res.ptr) +
-               (tl.nb * a.res.sn + dz * a.res.sd + ho * a.res.sh + wo * a.res.sw + tl.n0 + nt * 32 + 4 * hf);
-        if constexpr (EM & RE_MASK)
-          mp = reinterpret_cast<const H*>(a.msk.ptr) +
-               (tl.nb * a.msk.sn + dz * a.msk.sd + ho * a.msk.sh + wo * a.msk.sw + tl.n0 + nt * 32 + 4 * hf);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int co = tl.n0 + nt * 32 + 8 * g + 4 * hf;
-          if (co < a.cout) {
-            const float4 bs = *reinterpret_cast<const float4*>(lbias + co);
-            float v[4] = {fmaf(A[ms][4 * g + 0], osc, bs.x), fmaf(A[ms][4 * g + 1], osc, bs.y),
-                          fmaf(A[ms][4 * g + 2], osc, bs.z), fmaf(A[ms][4 * g + 3], osc, bs.w)};
-            if constexpr (EM & RE_RELU) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-            }
-            if constexpr (EM & RE_MASK) {
-              const uint2 mv = *reinterpret_cast<const uint2*>(mp + 8 * g);
-              float mm[4];
-              unpack_pk<H>(mv, mm);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = mm[e] > 0.f ? v[e] : 0.f;
-            }
-            if constexpr (EM & RE_RES) {
-              const uint2 rv = *reinterpret_cast<const uint2*>(rp + 8 * g);
-              float rr[4];
-              unpack_pk<H>(rv, rr);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] += rr[e];
-            }
-            if constexpr (EM & RE_BNRED) {
-              float vr[4], xb[4];
-              unpack_pk<H>(pack_pk<H, uint2>(v), vr);  // the stored (rounded) dz, as the separate reduce reads it
-              unpack_pk<H>(*reinterpret_cast<const uint2*>(reinterpret_cast<const H*>(a.bnx) +
-                                                          (yp - reinterpret_cast<H*>(a.y.ptr)) + 8 * g), xb);
-              const float4 c_sc = *reinterpret_cast<const float4*>(lbn + co);
-              const float4 c_sh = *reinterpret_cast<const float4*>(lbn + a.cout_pad + co);
-              const float4 c_mu = *reinterpret_cast<const float4*>(lbn + 2 * a.cout_pad + co);
-              const float4 c_is = *reinterpret_cast<const float4*>(lbn + 3 * a.cout_pad + co);
-              const float csc[4] = {c_sc.x, c_sc.y, c_sc.z, c_sc.w}, csh[4] = {c_sh.x, c_sh.y, c_sh.z, c_sh.w};
-              const float cmu[4] = {c_mu.x, c_mu.y, c_mu.z, c_mu.w}, cis[4] = {c_is.x, c_is.y, c_is.z, c_is.w};
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float dy = fmaf(xb[e], csc[e], csh[e]) > 0.f ? vr[e] : 0.f;
-                rs1[4 * g + e] += dy;
-                rs2[4 * g + e] = fmaf(dy, (xb[e] - cmu[e]) * cis[e], rs2[4 * g + e]);
-              }
-            }
-            if constexpr (EM & RE_ACC) {
-              float o[4];
-              unpack_pk<H>(*reinterpret_cast<const uint2*>(yp + 8 * g), o);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] += o[e];
-            }
-            *reinterpret_cast<uint2*>(yp + 8 * g) = pack_pk<H, uint2>(v);
-          }
-        }
-      }
-    }
-  };
-  // Transposed 2-D epilogue (output block nt of depth dz): per row ms the
-  // wave parks its fp32 accumulators (32 voxels x 32 channels) in LDS and
+  // Transposed epilogue (output block nt of depth dz; both forms): per row ms
+  // the wave parks its fp32 accumulators (32 voxels x 32 channels) in LDS and
   // reads them back as 8 consecutive channels of one voxel per lane, so every
-  // global access (output, residual, mask, accumulate) is 16 contiguous bytes
-  // and a wave instruction covers 16 voxels x 64 bytes -- instead of 32
-  // voxels x 8 bytes, which doubled the cost of a residual / mask operand.
+  // global access (output, residual, mask, accumulate, the BN input of
+  // RE_BNRED) is 16 contiguous bytes and a wave instruction covers 16 voxels
+  // x 64 bytes -- instead of 32 voxels x 8 bytes, which doubled the cost of a
+  // residual / mask operand in the 2-D form and of the BN input read in the
+  // fused 3-D data gradient (2.0 vs 1.24 ms per DUF launch, round 3).
   // The scratch is the wave's own DMA pieces 0-3 of the slot the next DMA
   // fills (free after the barrier; only this wave writes them, and only after
   // its flush): voxel v in piece v / 8, row v % 8 (128 bytes), 16-byte column
@@ -563,9 +508,29 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
           if constexpr (EM & RE_RELU) t[e] = fmaxf(t[e], 0.f);
           if constexpr (EM & RE_PRELU) t[e] = t[e] > 0.f ? t[e] : pslope * t[e];
         }
-        if (wo < a.y.w) {
+        if (wo < a.y.w && (KD == 1 || co < a.cout)) {  // (3-D: y->c % 8 == 0, whole 8-channel groups)
           H* yp = reinterpret_cast<H*>(a.y.ptr) + (tl.yo + dz * a.y.sd + (wave * RMS + ms) * a.y.sh + v * a.y.sw +
                                                    (SP == SP_Y ? a.spoff[(tl.n0 >> 5) + nt] : nt * 32) + 8 * tc8);
+          if constexpr (EM & RE_BNRED) {
+            float tr[8], xb[8];
+            Chunk<H>::unpack(Chunk<H>::pack(t), tr);  // the stored (rounded) dz, as the separate reduce reads it
+            Chunk<H>::unpack(*reinterpret_cast<const uint4*>(reinterpret_cast<const H*>(a.bnx) +
+                                                             (yp - reinterpret_cast<H*>(a.y.ptr))), xb);
+            float cst[4][8];  // scale, shift, mean, invstd of the lane's 8 channels
+#pragma unroll
+            for (int k4 = 0; k4 < 4; ++k4) {
+              const float4 c0 = *reinterpret_cast<const float4*>(lbn + k4 * a.cout_pad + co);
+              const float4 c1 = *reinterpret_cast<const float4*>(lbn + k4 * a.cout_pad + co + 4);
+              cst[k4][0] = c0.x; cst[k4][1] = c0.y; cst[k4][2] = c0.z; cst[k4][3] = c0.w;
+              cst[k4][4] = c1.x; cst[k4][5] = c1.y; cst[k4][6] = c1.z; cst[k4][7] = c1.w;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float dy = fmaf(xb[e], cst[0][e], cst[1][e]) > 0.f ? tr[e] : 0.f;
+              rs1[e] += dy;
+              rs2[e] = fmaf(dy, (xb[e] - cst[2][e]) * cst[3][e], rs2[e]);
+            }
+          }
           if constexpr (EM & RE_MASK) {
             uint4 mv;
             if constexpr (PREF) {
@@ -635,7 +600,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       for (int b = 0; b < 3; ++b) {
         if (all || b == bdone) {
           const int dz = P - (P + 3 - b) % 3;  // the output depth in bank b
-          if (dz >= tl.z0 && dz < tl.z1) epilogue(acc[b], tl, dz, 0, false);
+          if (dz >= tl.z0 && dz < tl.z1) epilogue_tr(acc[b], tl, dz, 0, false, scr);
 #pragma unroll
           for (int m = 0; m < RMS; ++m)
 #pragma unroll
@@ -644,26 +609,26 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       }
       if constexpr ((EM & RE_BNRED) != 0) {
         if (all) {
-          // the tile's partials: butterfly over the 32 voxel lanes of each
-          // half (fixed order), lane 0 / 32 writes its half's 16 channels
+          // the tile's partials: butterfly over the 16 lanes of each 8-channel
+          // column (lanes with equal lane & 3; fixed order); lanes 0-3 write
+          // [wave][sum: 32 channels | sum xhat: 32 channels] as 16-byte rows
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
+          for (int i = 0; i < 8; ++i) {
 #pragma unroll
-            for (int off = 1; off < 32; off <<= 1) {
+            for (int off = 4; off < 64; off <<= 1) {
               rs1[i] += __shfl_xor(rs1[i], off);
               rs2[i] += __shfl_xor(rs2[i], off);
             }
           }
-          if (r == 0) {
-            float* o = a.red_ws + ((int64_t)tl.t * RNW + wave) * 64 + hf * 32;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              o[i] = rs1[i];
-              o[16 + i] = rs2[i];
-            }
+          if (lane < 4) {
+            float4* o = reinterpret_cast<float4*>(a.red_ws + ((int64_t)tl.t * RNW + wave) * 64 + 8 * lane);
+            o[0] = make_float4(rs1[0], rs1[1], rs1[2], rs1[3]);
+            o[1] = make_float4(rs1[4], rs1[5], rs1[6], rs1[7]);
+            o[8] = make_float4(rs2[0], rs2[1], rs2[2], rs2[3]);
+            o[9] = make_float4(rs2[4], rs2[5], rs2[6], rs2[7]);
           }
 #pragma unroll
-          for (int i = 0; i < 16; ++i) rs1[i] = rs2[i] = 0.f;
+          for (int i = 0; i < 8; ++i) rs1[i] = rs2[i] = 0.f;
         }
       }
     } else {
@@ -818,20 +783,36 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
 
 // Channel c of the fused BN+ReLU backward reduce: the (tile, wave) partials
 // of the tiles whose output block holds c (tile order: block fastest), in a
-// fixed order, in double.  c = n0 + 8g + 4hf + e -> half hf, index 4g + e.
+// fixed order, in double.  A (tile, wave) record is [sum: 32 | sum xhat: 32]
+// over the block's channels.
 __global__ __launch_bounds__(256) void roll_bnred_final_kernel(const float* __restrict__ ws, int ntiles, int ntn,
                                                                int cout, float* __restrict__ o1,
                                                                float* __restrict__ o2) {
   const int c = blockIdx.x;
   if (c >= cout) return;
-  const int blk = c >> 5, cc = c & 31, hfc = (cc >> 2) & 1, idx = 4 * (cc >> 3) + (cc & 3);
+  const int blk = c >> 5, cc = c & 31;
   const int nt = (ntiles - blk + ntn - 1) / ntn;  // tiles blk, blk + ntn, ...
   double s1 = 0.0, s2 = 0.0;
-  for (int i = threadIdx.x; i < nt * RNW; i += 256) {
-    const int t = blk + ntn * (i / RNW), w = i % RNW;
-    const float* p = ws + ((int64_t)t * RNW + w) * 64 + hfc * 32;
-    s1 += p[idx];
-    s2 += p[16 + idx];
+  constexpr int U = 8;  // loads in flight per lane before the adds (the partials are latency-bound)
+  const int n = nt * RNW;
+  for (int i0 = threadIdx.x; i0 < n; i0 += 256 * U) {
+    float v1[U], v2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + 256 * u;
+      v1[u] = v2[u] = 0.f;
+      if (i < n) {
+        const int t = blk + ntn * (i / RNW), w = i % RNW;
+        const float* p = ws + ((int64_t)t * RNW + w) * 64;
+        v1[u] = p[cc];
+        v2[u] = p[32 + cc];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      s1 += v1[u];
+      s2 += v2[u];
+    }
   }
   __shared__ double r1[256], r2[256];
   r1[threadIdx.x] = s1;
@@ -943,7 +924,9 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   if (!k3 && !(d->kd == 1 && d->pd == 0 && y->c % 64 == 0)) return 0;
   // PReLU-backward mask (slope_ws): the mask has y's geometry and strides
   const bool pmask = slope_ws != nullptr;
-  if (d->bias_perm_r > 1 || (d->mask_slope && !pmask)) return 0;
+  if ((d->bias_perm_r > 1 && (y->shuffle != d->bias_perm_r || y->c % (d->bias_perm_r * d->bias_perm_r))) ||
+      (d->mask_slope && !pmask))
+    return 0;
   if (pmask) {
     if (!mask || !d->mask_slope || residual || d->kd != 1 || d->prologue) return 0;
     if (mask->dtype != y->dtype || mask->shuffle != y->shuffle || mask->n != y->n || mask->d != y->d ||
@@ -984,7 +967,7 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
            t->c == y->c && ((uintptr_t)t->ptr) % 8 == 0 && t->sn % 4 == 0 && t->sd % 4 == 0 && t->sh % 4 == 0 &&
            t->sw % 4 == 0;
   };
-  if (y->c % 4 != 0 || !out_ok(y)) return 0;
+  if (y->c % (k3 ? 8 : 4) != 0 || !out_ok(y)) return 0;
   if ((residual && !out_ok(residual)) || (mask && !pmask && !out_ok(mask))) return 0;
   for (const vsrk_tensor5* t : {x, y, residual, mask}) {  // every element offset fits in 32 bits
     if (!t) continue;
@@ -1011,6 +994,7 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   a.msk = rview(mask ? mask : y);
   a.w = w_packed;
   a.bias = bias;
+  a.bias_r = d->bias_perm_r > 1 ? d->bias_perm_r : 1;
   a.pro_scale = pro_scale;
   a.pro_shift = pro_shift;
   a.cin = x->c;

@@ -335,6 +335,94 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
   }
 }
 
+// The same sums as wgrad_reduce_kernel, in dw's memory order: a workgroup
+// owns one (output channel, input block of cit_w channels, kd) and its
+// cit_w x taps outputs, reads each split's [tap][ci] rows of the slab
+// coalesced (8 splits of loads in flight per output), sums the splits in
+// order 0, 1, 2, ... in fp32, and writes the (ci, tap) run of dw through LDS.
+// Workgroups past the weights sum the dbias tails, one output channel per
+// lane.  (wgrad_reduce_kernel writes dw with a 9-float stride per lane: the
+// DRF sub-pixel weight gradients spent ~27 us per reduce in it.)
+__global__ __launch_bounds__(256) void wgrad_reduce_rows_kernel(
+    const float* __restrict__ ws, float* __restrict__ dw, float* __restrict__ db, int nsplit, int slab, int cout,
+    int cin, int kd, int taps2, int nco_t, int nci_t, int cot_w, int cit_w, int kd_bias, int perm_r, float scale,
+    int accumulate, int nblk_w) {
+  constexpr int U = 8;
+  __shared__ float out[64 * 9];
+  const int64_t sstride = (int64_t)nco_t * nci_t * kd * slab;
+  const int tid = threadIdx.x;
+  auto sum_splits = [&](const float* p) __attribute__((always_inline)) {
+    float s = 0.f;
+    for (int k0 = 0; k0 < nsplit; k0 += U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = k0 + u < nsplit ? p[(int64_t)(k0 + u) * sstride] : 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u) s += v[u];
+    }
+    return s;
+  };
+  auto torch_co = [&](int co) __attribute__((always_inline)) {
+    if (perm_r > 1) {
+      const int rr = perm_r * perm_r, cp = cout / rr;
+      const int sub = co / cp;
+      return (co - sub * cp) * rr + sub;
+    }
+    return co;
+  };
+  if ((int)blockIdx.x >= nblk_w) {  // dbias
+    if (!db) return;
+    const int co = ((int)blockIdx.x - nblk_w) * 256 + tid;
+    if (co >= cout) return;
+    const int combo = (kd_bias * nci_t + 0) * nco_t + co / cot_w;
+    const float s = sum_splits(ws + (int64_t)combo * slab + (int64_t)taps2 * cot_w * cit_w + (co % cot_w)) * scale;
+    const int cot = torch_co(co);
+    db[cot] = accumulate ? db[cot] + s : s;
+    return;
+  }
+  int b = blockIdx.x;
+  const int kdi = b % kd;
+  b /= kd;
+  const int cic = b % nci_t;
+  const int co = b / nci_t;
+  const int ci0 = cic * cit_w;
+  const int nci = min(cit_w, cin - ci0);
+  const int nout = nci * taps2;
+  const int combo = (kdi * nci_t + cic) * nco_t + co / cot_w;
+  const float* base = ws + (int64_t)combo * slab + (int64_t)(co % cot_w) * cit_w;
+  for (int j = tid; j < cit_w * taps2; j += 256) {  // read order: tap-major rows of cit_w input channels
+    const int tap = j / cit_w, cil = j - tap * cit_w;
+    if (cil < nci) out[cil * taps2 + tap] = sum_splits(base + (int64_t)tap * cot_w * cit_w + cil) * scale;
+  }
+  __syncthreads();
+  float* d = dw + ((int64_t)torch_co(co) * cin + ci0) * kd * taps2 + (int64_t)kdi * taps2;
+  for (int j = tid; j < nout; j += 256) {  // dw order: (ci, [kd,] tap)
+    const int cil = j / taps2, tap = j - cil * taps2;
+    float* q = d + (int64_t)cil * kd * taps2 + tap;
+    *q = accumulate ? *q + out[j] : out[j];
+  }
+}
+
+// the row-order reduce where it fits; VSRK_WGRAD_REDUCE=0 keeps the per-output kernel (A/B)
+static bool wgrad_reduce_rows(const float* ws, float* dw, float* db, int nsplit, int slab, int cout, int cin, int kd,
+                              int taps2, int nco_t, int nci_t, int cot_w, int cit_w, int kd_bias, int perm_r,
+                              float scale, int accumulate, hipStream_t s) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("VSRK_WGRAD_REDUCE");
+    mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  const int nblk_w = cout * nci_t * kd;
+  // one lane sums all splits of an output: only for few splits and enough
+  // workgroups (EDSR's 64 -> 64 has 256 splits over 64 such workgroups)
+  if (!mode || cit_w * taps2 > 64 * 9 || nsplit > 32 || nblk_w < 256) return false;
+  const int nblk_b = db ? (int)ceil_div64(cout, 256) : 0;
+  wgrad_reduce_rows_kernel<<<nblk_w + nblk_b, 256, 0, s>>>(ws, dw, db, nsplit, slab, cout, cin, kd, taps2, nco_t,
+                                                            nci_t, cot_w, cit_w, kd_bias, perm_r, scale, accumulate,
+                                                            nblk_w);
+  return true;
+}
+
 }  // namespace
 struct WgradPlan {
   int nco, nci;            // channel blocks per workgroup (x32)
@@ -434,9 +522,11 @@ extern "C" int vsrk_conv_wgrad(const vsrk_conv_desc* d, const vsrk_tensor5* x, c
       VSRK_LAUNCH_CHECK("conv_wgrad(roll)");
       const int nci = x->c / 32, nco = dy->c / 32;
       const int64_t total = (int64_t)dy->c * x->c * 27 + (dbias ? dy->c : 0);
-      wgrad_reduce_kernel<<<(int)ceil_div64(total, 64), 256, 0, s>>>(
-          (const float*)workspace, dw, dbias, 2 * ns, 3 * nci * nco, 9 * 1024 + 32, dy->c, x->c, 3, 3, 3, nco, nci, 32,
-          32, std::min(d->pd, 2), perm_r, dy_scale, accumulate);
+      if (!wgrad_reduce_rows((const float*)workspace, dw, dbias, 2 * ns, 9 * 1024 + 32, dy->c, x->c, 3, 9, nco, nci,
+                             32, 32, std::min(d->pd, 2), perm_r, dy_scale, accumulate, s))
+        wgrad_reduce_kernel<<<(int)ceil_div64(total, 64), 256, 0, s>>>(
+            (const float*)workspace, dw, dbias, 2 * ns, 3 * nci * nco, 9 * 1024 + 32, dy->c, x->c, 3, 3, 3, nco, nci,
+            32, 32, std::min(d->pd, 2), perm_r, dy_scale, accumulate);
       VSRK_LAUNCH_CHECK("conv_wgrad_reduce");
       return VSRK_OK;
     }
@@ -500,9 +590,12 @@ extern "C" int vsrk_conv_wgrad(const vsrk_conv_desc* d, const vsrk_tensor5* x, c
   }
   VSRK_LAUNCH_CHECK("conv_wgrad");
   const int64_t total = (int64_t)dy->c * x->c * d->kd * d->kh * d->kw + (dbias ? dy->c : 0);
-  wgrad_reduce_kernel<<<(int)ceil_div64(total, 64), 256, 0, s>>>(
-      (const float*)workspace, dw, dbias, p.nsplit, p.ncombos, p.slab, dy->c, x->c, d->kd, d->kh, d->kw,
-      p.n_co_tiles, p.n_ci_chunks, 32 * p.nco, 32 * p.nci, a.kd_bias, perm_r, dy_scale, accumulate);
+  if (!wgrad_reduce_rows((const float*)workspace, dw, dbias, p.nsplit, p.slab, dy->c, x->c, d->kd, d->kh * d->kw,
+                         p.n_co_tiles, p.n_ci_chunks, 32 * p.nco, 32 * p.nci, a.kd_bias, perm_r, dy_scale, accumulate,
+                         s))
+    wgrad_reduce_kernel<<<(int)ceil_div64(total, 64), 256, 0, s>>>(
+        (const float*)workspace, dw, dbias, p.nsplit, p.ncombos, p.slab, dy->c, x->c, d->kd, d->kh, d->kw,
+        p.n_co_tiles, p.n_ci_chunks, 32 * p.nco, 32 * p.nci, a.kd_bias, perm_r, dy_scale, accumulate);
   VSRK_LAUNCH_CHECK("conv_wgrad_reduce");
   return VSRK_OK;
 }

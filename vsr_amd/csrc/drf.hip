@@ -131,14 +131,21 @@ __global__ __launch_bounds__(256) void prelu_partial_kernel(View y, View dx, int
   if (threadIdx.x == 0) part[blockIdx.x] = sh[0];
 }
 
-__global__ void prelu_final_kernel(const double* __restrict__ part, int nblk, const float* __restrict__ a,
-                                   float* __restrict__ da, int accumulate) {
-  __shared__ double sh[256];
+// 1024 lanes, both of a lane's partials loaded before the adds (a 256-lane
+// loop over the 2048 partials was a chain of 8 dependent loads per lane)
+__global__ __launch_bounds__(1024) void prelu_final_kernel(const double* __restrict__ part, int nblk,
+                                                           const float* __restrict__ a, float* __restrict__ da,
+                                                           int accumulate) {
+  __shared__ double sh[1024];
   double s = 0.0;
-  for (int b = threadIdx.x; b < nblk; b += blockDim.x) s += part[b];
+  for (int b = threadIdx.x; b < nblk; b += 2048) {
+    const double p0 = part[b];
+    const double p1 = b + 1024 < nblk ? part[b + 1024] : 0.0;
+    s += p0 + p1;
+  }
   sh[threadIdx.x] = s;
   __syncthreads();
-  for (int k = 128; k > 0; k >>= 1) {
+  for (int k = 512; k > 0; k >>= 1) {
     if (threadIdx.x < k) sh[threadIdx.x] += sh[threadIdx.x + k];
     __syncthreads();
   }
@@ -201,7 +208,7 @@ extern "C" int vsrk_prelu_wgrad(const vsrk_tensor5* y, const vsrk_tensor5* dx, c
   else
     prelu_partial_kernel<float><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vd, nvox, part);
   VSRK_LAUNCH_CHECK("prelu_partial");
-  prelu_final_kernel<<<1, 256, 0, s>>>(part, PRELU_BLOCKS, a, da, accumulate);
+  prelu_final_kernel<<<1, 1024, 0, s>>>(part, PRELU_BLOCKS, a, da, accumulate);
   VSRK_LAUNCH_CHECK("prelu_final");
   return VSRK_OK;
 }
@@ -369,7 +376,7 @@ extern "C" int vsrk_prelu_bwd(const vsrk_tensor5* y, const vsrk_tensor5* dy, con
   else
     prelu_bwd_kernel<float><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, (int)nr64, vec, part);
   VSRK_LAUNCH_CHECK("prelu_bwd");
-  prelu_final_kernel<<<1, 256, 0, s>>>(part, PRELU_BLOCKS, a, da, accumulate_da);
+  prelu_final_kernel<<<1, 1024, 0, s>>>(part, PRELU_BLOCKS, a, da, accumulate_da);
   VSRK_LAUNCH_CHECK("prelu_final");
   return VSRK_OK;
 }

@@ -86,7 +86,7 @@ class GradSync:
         for b, h in enumerate(self._handles):
             self._handles[b].wait()
         f = unscale if self._avg else unscale / self.world
-        if unscale != 1.0:
+        if getattr(self.net, "compute_dtype", None) == torch.float16:
             # fp16: unscale and flag inf / NaN in one pass over the buckets; an
             # overflow on any rank reaches every rank through the all-reduce,
             # so every rank skips the same step (BaseNet.step_ok)
@@ -116,8 +116,13 @@ class SyncBNAllReduce:
     per BN layer, at most 2 x 256 floats).  The global voxel count of a layer
     is its depth times the sum over ranks of N*H*W of the step's input
     (ranks may hold batches of different sizes: uncropped slices, a last
-    partial batch): ``global_count(local)`` all-reduces that once per forward
-    (one host read per step), and the net scales every layer's count by it."""
+    partial batch): ``global_count(local, device)`` all-reduces that once per
+    forward into a float64 DEVICE scalar, stream-ordered, and never reads it
+    on the host: the BN kernels take the count from device memory
+    (vsrk_bn_finalize_dcount) and the backward divides its all-reduced sums
+    by the count on the device (duf_net._ScaledWork).  So a DUF training step
+    has no host synchronisation on the count at any step, whatever the
+    ranks' batch shapes."""
 
     def __init__(self, group=None):
         self.group = group
@@ -132,12 +137,18 @@ class SyncBNAllReduce:
         kernels queued in between (a weight gradient) hide the collective."""
         return dist.all_reduce(t, group=self.group, async_op=True)
 
-    def global_count(self, local: int) -> int:
-        """Sum of `local` over the ranks (exact in float64 up to 2^53)."""
-        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(self.group) == "nccl" else "cpu"
-        t = torch.tensor([float(local)], dtype=torch.float64, device=dev)
+    def global_count(self, local: int, device) -> torch.Tensor:
+        """Sum of `local` over the ranks as a float64 scalar on `device`
+        (exact up to 2^53).  RCCL: an async all-reduce whose wait() only
+        orders the current stream -- no host read.  gloo (CPU tensors) blocks
+        the host, as every gloo collective does."""
+        if dist.get_backend(self.group) == "nccl":
+            t = torch.full((1,), float(local), dtype=torch.float64, device=device)
+            dist.all_reduce(t, group=self.group, async_op=True).wait()
+            return t
+        t = torch.full((1,), float(local), dtype=torch.float64)
         dist.all_reduce(t, group=self.group)
-        return int(t.item())
+        return t.to(device)
 
 
 def enable_sync_bn(net, group=None) -> bool:

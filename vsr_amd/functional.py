@@ -35,14 +35,23 @@ class KernelTimer:
     yv)`` sees the launch kind (("conv_fwd" | "conv_wgrad", (kd, kh, kw))) and
     its logical views (vsrk_tensor5: for a weight gradient the input and the
     output gradient) and returns the launch's algorithmic FLOP, or 0 to skip
-    it.  bench.py uses it for the roofline of the dominant conv."""
+    it.  Each timed launch is labelled by direction: "wgrad" for a weight
+    gradient, else "fwd" or "dgrad" by ``phase``, which the caller sets to
+    "fwd" before the forward and "bwd" before the backward.  Every conv entry point that can run
+    a roofline kernel goes through ``wrap`` -- the plain conv, the fused conv +
+    reduction (conv_reduce) and the fused conv + PReLU backward
+    (conv_prelu_bwd) -- so a fused data gradient is timed like the unfused one.
+    bench.py uses it for the roofline of the dominant conv."""
 
     def __init__(self, match):
         self.match = match
-        self.events: list[tuple[torch.cuda.Event, torch.cuda.Event, float]] = []
+        self.events: list[tuple[torch.cuda.Event, torch.cuda.Event, float, str]] = []
         self.enabled = True
+        self.phase = "fwd"
 
-    def wrap(self, kind, xv, yv, launch):
+    def wrap(self, kind, xv, yv, launch, launched=lambda rc: True):
+        """launch() -> status; ``launched(status)`` False means nothing ran
+        (a fused entry point reporting "not eligible"): the events are dropped."""
         flop = self.match(kind, xv, yv) if self.enabled else 0
         if not flop:
             return launch()
@@ -50,14 +59,20 @@ class KernelTimer:
         s.record()
         out = launch()
         e.record()
-        self.events.append((s, e, float(flop)))
+        if launched(out):
+            label = "wgrad" if kind[0] == "conv_wgrad" else ("dgrad" if self.phase == "bwd" else "fwd")
+            self.events.append((s, e, float(flop), label))
         return out
 
-    def totals(self) -> tuple[float, float, int]:
-        """(total FLOP, total seconds, launches) of the matched launches."""
+    def totals(self, label: str | None = None) -> tuple[float, float, int]:
+        """(total FLOP, total seconds, launches) of the matched launches [of one direction]."""
         torch.cuda.synchronize()
-        t = sum(s.elapsed_time(e) for s, e, _ in self.events) * 1e-3
-        return sum(f for _, _, f in self.events), t, len(self.events)
+        ev = [x for x in self.events if label is None or x[3] == label]
+        t = sum(s.elapsed_time(e) for s, e, _, _ in ev) * 1e-3
+        return sum(f for _, _, f, _ in ev), t, len(ev)
+
+    def labels(self) -> list[str]:
+        return [d for d in ("fwd", "dgrad", "wgrad") if any(x[3] == d for x in self.events)]
 
     def mean_ms(self) -> float:
         flop, t, n = self.totals()
@@ -199,6 +214,10 @@ def conv(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, *, bias: to
 FUSE = os.environ.get("VSRK_FUSE", "1") != "0"
 
 
+def _launched(rc) -> bool:
+    return rc != 2  # VSRK_ERR_UNSUPPORTED: the fused entry point launched nothing
+
+
 def conv_prelu_bwd(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, y_fwd: torch.Tensor,
                    a: torch.Tensor, da: torch.Tensor, accumulate_da: bool, *, x_shuffle: int = 1, y_shuffle: int = 1,
                    subpixel: int = 0) -> bool:
@@ -211,9 +230,13 @@ def conv_prelu_bwd(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, y
     d = _desc(k, pad, mask_slope=a, subpixel=subpixel)
     xv, yv, mv = N.t5(x, x_shuffle), N.t5(y, y_shuffle), N.t5(y_fwd, y_shuffle)
     ws = workspace(lib.vsrk_conv_prelu_bwd_workspace(), y.device)
-    rc = lib.vsrk_conv_fwd_prelu_bwd(C.byref(d), C.byref(xv), wp.data_ptr(), None, C.byref(mv), C.byref(yv),
-                                     da.data_ptr(), 1 if accumulate_da else 0, ws.data_ptr(), ws.numel(),
-                                     N.stream_ptr(y.device))
+
+    def launch():
+        return lib.vsrk_conv_fwd_prelu_bwd(C.byref(d), C.byref(xv), wp.data_ptr(), None, C.byref(mv), C.byref(yv),
+                                           da.data_ptr(), 1 if accumulate_da else 0, ws.data_ptr(), ws.numel(),
+                                           N.stream_ptr(y.device))
+
+    rc = (timer.wrap(("conv_fwd", tuple(k)), xv, yv, launch, _launched) if timer is not None else launch())
     if rc == 2:  # VSRK_ERR_UNSUPPORTED
         return False
     N.check(rc, "conv_fwd_prelu_bwd")
@@ -242,11 +265,15 @@ def conv_reduce(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, *, bias: tor
     xv, yv = N.t5(x), N.t5(y)
     ws = workspace(lib.vsrk_conv_fwd_reduce_workspace(C.byref(d), C.byref(yv)), y.device)
     bv = N.t5(bnx) if bnx is not None else None
-    rc = lib.vsrk_conv_fwd_reduce(C.byref(d), C.byref(xv), wp.data_ptr(), N.ptr(bias), N.ptr(pro_scale),
-                                  N.ptr(pro_shift), C.byref(yv), mode, C.byref(bv) if bv is not None else None,
-                                  *(st[i].data_ptr() if st is not None else None for i in range(4)),
-                                  out[0].data_ptr(), out[1].data_ptr(), ws.data_ptr(), ws.numel(),
-                                  N.stream_ptr(y.device))
+
+    def launch():
+        return lib.vsrk_conv_fwd_reduce(C.byref(d), C.byref(xv), wp.data_ptr(), N.ptr(bias), N.ptr(pro_scale),
+                                        N.ptr(pro_shift), C.byref(yv), mode, C.byref(bv) if bv is not None else None,
+                                        *(st[i].data_ptr() if st is not None else None for i in range(4)),
+                                        out[0].data_ptr(), out[1].data_ptr(), ws.data_ptr(), ws.numel(),
+                                        N.stream_ptr(y.device))
+
+    rc = (timer.wrap(("conv_fwd", tuple(k)), xv, yv, launch, _launched) if timer is not None else launch())
     if rc == 2:  # VSRK_ERR_UNSUPPORTED
         return None
     N.check(rc, "conv_fwd_reduce")
@@ -477,11 +504,21 @@ def bn_relu_bwd_apply_multi(x: torch.Tensor, dx: torch.Tensor, accumulate: bool,
 
 
 def bn_finalize(sums: torch.Tensor, count: float, gamma, beta, eps: float, momentum: float,
-                running_mean=None, running_var=None) -> torch.Tensor:
-    """-> (4, C) fp32: scale, shift, mean, invstd (running stats updated in place)."""
+                running_mean=None, running_var=None, count_dev: torch.Tensor | None = None) -> torch.Tensor:
+    """-> (4, C) fp32: scale, shift, mean, invstd (running stats updated in place).
+    count_dev: a float64 device scalar; the voxel count is then count *
+    count_dev, read by the kernel (no host synchronisation)."""
     lib = _lib()
     c = sums.shape[1]
     out = torch.empty((4, c), dtype=torch.float32, device=sums.device)
+    if count_dev is not None:
+        assert count_dev.dtype == torch.float64 and count_dev.device == sums.device
+        N.check(lib.vsrk_bn_finalize_dcount(sums[0].data_ptr(), sums[1].data_ptr(), count_dev.data_ptr(),
+                                            float(count), N.ptr(gamma), N.ptr(beta), float(eps), float(momentum),
+                                            N.ptr(running_mean), N.ptr(running_var), out[0].data_ptr(),
+                                            out[1].data_ptr(), out[2].data_ptr(), out[3].data_ptr(), c,
+                                            N.stream_ptr(sums.device)), "bn_finalize_dcount")
+        return out
     N.check(lib.vsrk_bn_finalize(sums[0].data_ptr(), sums[1].data_ptr(), float(count), N.ptr(gamma), N.ptr(beta),
                                  float(eps), float(momentum), N.ptr(running_mean), N.ptr(running_var),
                                  out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), out[3].data_ptr(), c,

@@ -154,7 +154,8 @@ class BaseNet(nn.Module):
         found = bool(f.item())
         if self.loss_scale is None and self._scale is not None:
             if found:
-                self._scale = max(self._scale * 0.5, 1.0)
+                # no floor (GradScaler): the check below keeps running at any scale
+                self._scale = self._scale * 0.5
                 self._good_steps = 0
             else:
                 self._good_steps += 1
@@ -222,8 +223,10 @@ class _TapeFunction(torch.autograd.Function):
         g = net._backward(ctx.tape, grads if len(grads) > 1 else grads[0])
         net._join_wgrad()
         ctx.tape = None
-        if scale != 1.0 and net._grad_sink is None:
+        if net.compute_dtype == torch.float16 and net._grad_sink is None:
             # unscale every parameter gradient and flag any inf / NaN (one fused
-            # pass; the data-parallel path does this on its buckets in GradSync.finish)
+            # pass; the data-parallel path does this on its buckets in
+            # GradSync.finish).  fp16 always checks, at scale 1 too: an
+            # overflow is not a property of the scale alone
             net._found_inf = unscale_check([t for t in g.values()], 1.0 / scale)
         return (None, None, *[g.get(id(p)) for p in ctx.params])

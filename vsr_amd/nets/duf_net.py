@@ -63,6 +63,19 @@ class _DenseLayer(nn.Module):
         self.tail.add_module("conv", nn.Conv3d(tail_in, 256, kernel_size=(1, 3, 3), padding=(0, 1, 1)))
 
 
+class _ScaledWork:
+    """A SyncBN backward all-reduce in flight: wait() orders the stream after
+    it and then divides the summed (sum_dy, sum_dy_xhat) by the global count
+    on the device, so the apply runs with count 1."""
+
+    def __init__(self, work, red, count_dev, mult):
+        self.work, self.red, self.count_dev, self.mult = work, red, count_dev, mult
+
+    def wait(self):
+        self.work.wait()
+        self.red.div_(self.count_dev.to(torch.float32) * self.mult)
+
+
 class DUFNet(BaseNet):
     """Dynamic Upsampling Filter network (MISR: list of T (B,C,h,w) -> (B,C,rh,rw))."""
 
@@ -106,16 +119,20 @@ class DUFNet(BaseNet):
             sums = F.bn_stats(x)
         else:
             sums = sums.clone()  # the SyncBN hook all-reduces in place
-        count = x.shape[0] * x.shape[1] * x.shape[2] * x.shape[3]
+        count, count_dev = x.shape[0] * x.shape[1] * x.shape[2] * x.shape[3], None
         if self.bn_allreduce is not None:
             self.bn_allreduce(sums)
-            count = x.shape[1] * self._global_nhw  # depth x the N*H*W of every rank
+            # depth x the N*H*W of every rank, a device scalar (no host read)
+            count, count_dev = x.shape[1], self._global_nhw
         st = F.bn_finalize(sums, count, bn.weight, bn.bias, bn.eps, bn.momentum if bn.momentum is not None else 0.1,
                            bn.running_mean if bn.track_running_stats else None,
-                           bn.running_var if bn.track_running_stats else None)
+                           bn.running_var if bn.track_running_stats else None, count_dev=count_dev)
         if bn.track_running_stats and bn.num_batches_tracked is not None:
             bn.num_batches_tracked.add_(1)
-        st.count = count
+        # the backward's apply takes 1 / count: SyncBN hands it sums already
+        # divided by the device count (_bn_backward_reduce) and count 1
+        st.count = count if count_dev is None else 1.0
+        st.count_dev = (count_dev, float(count)) if count_dev is not None else None
         return st
 
     def _bn_backward_reduce(self, bn, x, dz, st, grads, red=None):
@@ -138,7 +155,7 @@ class DUFNet(BaseNet):
         work = None
         if self.bn_allreduce is not None and st.count != float("inf"):
             red = red.clone()
-            work = self.bn_allreduce.start(red)
+            work = _ScaledWork(self.bn_allreduce.start(red), red, *st.count_dev)
         self._grad_done(grads, bn.weight, gw)
         self._grad_done(grads, bn.bias, gb)
         return red, work
@@ -159,7 +176,7 @@ class DUFNet(BaseNet):
             # the reference's residual branch squeezes depth 1 (duf_net.py:94-96) and only works for T = 7
             raise RuntimeError(f"DUFNet needs num_frames = 7 (got {T}): depth after the dense layer must be 1")
         if self.training and self.bn_allreduce is not None:
-            self._global_nhw = self.bn_allreduce.global_count(n * h * w)  # SyncBN: the global batch
+            self._global_nhw = self.bn_allreduce.global_count(n * h * w, dev)  # SyncBN: the global batch
         frames = torch.stack(inputs, dim=2)  # (n, cin, T, h, w) fp32
         xv = F.to_view(frames, cd, cpad=8)[..., :cin]  # (n, T, h, w, cin), chunk-aligned storage
         C = torch.empty((n, T, h, w, ctot), dtype=cd, device=dev)
