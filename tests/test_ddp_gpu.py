@@ -14,9 +14,11 @@ one GPU per rank).
     global voxel count comes from the device-side count all-reduce
     (SyncBNAllReduce.global_count).  Each rank's mean loss is weighted by
     its share of the global batch (x world, GradSync averages), so the
-    averaged gradient is the gradient of the global mean.  Same-precision
-    single process as the yardstick: bf16 roundings move with the summation
-    order of the statistics, so gradients rel-L2 <= 3e-2, outputs <= 3e-2.
+    averaged gradient is the gradient of the global mean.  Yardstick: one
+    fp32 process on the whole batch; every gradient of the two bf16 ranks
+    must be within twice the distance of one bf16 process from it (bf16
+    roundings move with the summation order of the statistics), outputs
+    within 5e-2.
   * fp16 overflow on ONE rank (its loss scale forced to 2^40): the inf
     reaches every rank through the bucket all-reduce and both ranks skip
     the step (GradSync.finish -> BaseNet.step_ok).
@@ -153,22 +155,26 @@ def test_fp16_overflow_on_one_rank_skips_on_both():
 
 
 def test_duf_bf16_uneven_shards_equal_one_process():
-    ref = _single("duf", "bf16")
+    ref32 = _single("duf", "fp32")  # the yardstick
+    ref16 = _single("duf", "bf16")  # how far one bf16 process lands from it
     got = _run_ranks("duf", precision="bf16", split=SPLIT["uneven"])
-    gmax = max(v.norm().item() for v in ref["grads"].values())
+    gmax = max(v.norm().item() for v in ref32["grads"].values())
     for rank in (0, 1):
         g_r = {k: torch.from_numpy(v) for k, v in got[rank]["grads"].items()}
-        for k, g in ref["grads"].items():
+        for k, g in ref32["grads"].items():
             if g.norm().item() <= 1e-6 * gmax:
                 assert g_r[k].norm().item() <= 1e-2 * gmax, (rank, k)
                 continue
-            rel = (g_r[k] - g).norm().item() / g.norm().item()
-            assert rel <= 3e-2, (rank, k, rel)
-        for k, v in ref["buffers"].items():
+            e_ddp = (g_r[k] - g).norm().item() / g.norm().item()
+            e_one = (ref16["grads"][k] - g).norm().item() / g.norm().item()
+            # bf16 noise: within twice the single bf16 process's own error (a
+            # missing or doubled reduction over a shard is an O(1) error)
+            assert e_ddp <= max(2 * e_one, 1e-2), (rank, k, e_ddp, e_one)
+        for k, v in ref32["buffers"].items():
             b = torch.from_numpy(got[rank]["buffers"][k])
-            assert (b - v).abs().max().item() <= 1e-3 * (1 + v.abs().max().item()), k
-        exp = _shard_split(ref["out"], rank, SPLIT["uneven"])
-        assert (torch.from_numpy(got[rank]["out"]) - exp).abs().max().item() <= 3e-2, rank
+            assert (b - v).abs().max().item() <= 2e-3 * (1 + v.abs().max().item()), k
+        exp = _shard_split(ref32["out"], rank, SPLIT["uneven"])
+        assert (torch.from_numpy(got[rank]["out"]) - exp).abs().max().item() <= 5e-2, rank
 
 
 @pytest.mark.parametrize("model", ["duf", "drf"])

@@ -73,6 +73,7 @@ def main():
               "fwdpro": x.numel() // x.shape[-1] * (ci * 2) + y.numel() * esz[y.dtype],
               "wgradpro": x.numel() // x.shape[-1] * (ci * 2) + gy.numel() // gy.shape[-1] * (co * 2),
               "wgrad": x.numel() // x.shape[-1] * (ci * 2) + gy.numel() // gy.shape[-1] * (co * 2)}
+    nbytes["dgradred"] = nbytes["dgrad"] + dx.numel() * esz[dx.dtype]
     dw = torch.empty((co, ci, *k), device=dev)
     db = torch.empty(co, device=dev)
     wp = F.pack_weight(wt, 0, dt)
@@ -90,7 +91,12 @@ def main():
         "wgradpro": lambda: F.conv_wgrad(x, gy, k, pad, dw, db, prologue=F.PRO_AFFINE_RELU, pro_scale=psc,
                                          pro_shift=psh),
         "dgrad": lambda: F.conv(gy, wp1, dx, k, dpad),
+        # the fused form DUF runs (bn2's backward reduce in the data gradient's store pass)
+        "dgradred": lambda: F.conv_reduce(gy, wp1, dx, bnx=bnx, st=st, k=k, pad=dpad),
     }
+    bnx = torch.randn((n, d, h, w, ci), generator=g).to(dev, dt) if ci >= 8 else None
+    st = torch.stack([torch.rand(ci, generator=g) + 0.5, torch.randn(ci, generator=g) * 0.1,
+                      torch.randn(ci, generator=g) * 0.1, torch.rand(ci, generator=g) + 0.5]).to(dev)
     for name in args.what.split(","):
         fn = cases[name]
         for _ in range(3):

@@ -54,6 +54,35 @@ constexpr int RCH = 16;                    // input channels per stage
 constexpr int RNAI = (RHROWS + 31) / 32;   // 20 A pieces (32 voxels x 32 B each)
 constexpr int RNA = (RNAI + RNW - 1) / RNW;  // 3: A pieces per wave (q < 3)
 constexpr int RNSLOT = 3;
+// Ablation builds for measurements only (tools/build_exp_multi.sh ... -DROLL_ABL=n;
+// results are wrong): 1 no MFMAs, 2 no DMA pieces, 4 no epilogue, 8 no
+// fragment reads, 16 no stage barrier
+#ifndef ROLL_ABL
+#define ROLL_ABL 0
+#endif
+// ROLL_LEAN (default 1): cheaper DMA piece issue -- M0 set without saving /
+// restoring it (nothing else in these kernels uses M0: checked in the ISA),
+// the zero page address held in a VGPR pair instead of re-materialised per
+// piece, the A / B role of a piece resolved at compile time where every wave
+// agrees, and every stage issues its pieces unconditionally (zero-page pieces
+// past the end of the walk) so each wait is one compile-time vmcnt with no
+// branch; 0 builds the previous form for A/B
+#ifndef ROLL_LEAN
+#define ROLL_LEAN 1
+#endif
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void glds16_m0(const void* gsrc, uint32_t lds_base) {
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %0, off"
+      :
+      : "v"(gsrc), "s"(lds_base)
+      : "memory", "m0");
+}
+#pragma clang diagnostic pop
 
 // Geometry of the two forms.  KD = 3, NT = 1: Conv3d 3x3x3, one 32-channel
 // output block, three accumulator banks (output depths).  KD = 1, NT = 2:
@@ -152,7 +181,9 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   constexpr int RNQ = G::NQ, RSLOT = G::SLOT, NACC = G::NACC;
   // the residual / mask operand of a 2-D tile is loaded into registers during
   // its last stage (one extra operand, no accumulate)
-  constexpr bool PREF = KD == 1 && ((EM & RE_RES) != 0) != ((EM & RE_MASK) != 0) && !(EM & RE_ACC);
+  // (3-D: the BN input of RE_BNRED, read by the flush of the slice's finished depth)
+  constexpr bool PREF = (KD == 1 && ((EM & RE_RES) != 0) != ((EM & RE_MASK) != 0) && !(EM & RE_ACC)) ||
+                        (KD == 3 && (EM & RE_BNRED) != 0);
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -201,7 +232,10 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // the channel.  qa: the wave's A pieces (bit q); qkd[kd]: its B pieces of
   // taps of depth kd.
   int rel[RNQ], hwv[RNQ];
-  unsigned qa = 0, qkd0 = 0, qkd1 = 0, qkd2 = 0;
+  // qa in closed form: pieces q < RNAI / RNW are A pieces on every wave, so
+  // the compiler resolves their role at compile time
+  const unsigned qa = ((1u << (RNAI / RNW)) - 1) | (wave < RNAI % RNW ? 1u << (RNAI / RNW) : 0u);
+  unsigned qkd0 = 0, qkd1 = 0, qkd2 = 0;
 #pragma unroll
   for (int q = 0; q < RNQ; ++q) {
     const int j = wave + RNW * q;
@@ -213,7 +247,6 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       const int p = (lane & 1) ^ ((ww >> 3) & 1);
       rel[q] = hh * a.x.sh + ww * a.x.sw + 8 * p;
       hwv[q] = v < RHROWS ? ((hh << 8) | ww) : -1;
-      qa |= 1u << q;
     } else if (j < G::NI) {
       const int co = lane >> 1;
       const int p = (lane & 1) ^ ((co >> 3) & 1);
@@ -306,6 +339,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     return true;
   };
   const char* zp = reinterpret_cast<const char*>(g_roll_zero);
+  if constexpr (ROLL_LEAN) asm volatile("" : "+v"(zp));  // keep the zero page address in VGPRs
   struct Dma {
     const H* xb;
     const H* wsrc;
@@ -328,7 +362,10 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     const int j = wave + RNW * q;
     const H* base = ((qa >> q) & 1) ? d.xb : d.wsrc;
     const void* src = ((d.use >> q) & 1) ? (const void*)(base + rel[q]) : (const void*)zp;
-    glds16(src, lds_addr(lds) + slot * RSLOT + j * 1024);
+    if constexpr (!(ROLL_ABL & 2)) {
+      if constexpr (ROLL_LEAN) glds16_m0(src, lds_addr(lds) + slot * RSLOT + j * 1024);
+      else glds16(src, lds_addr(lds) + slot * RSLOT + j * 1024);
+    }
   };
 
   f32x16 acc[NACC][RMS];  // KD 3: bank b holds the output depth dz with dz % 3 == b; KD 1: output block b
@@ -361,7 +398,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // flush's barrier.
   typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
   u32x4_t pre[PREF ? RMS : 1][PREF ? NT : 1][2];
-  const RView& pv = (EM & RE_RES) ? a.res : a.msk;
+  const RView& pv = (EM & RE_RES) ? a.res : a.msk;  // (RE_BNRED: msk is the BN input view)
   const int tv = lane >> 2, tc8 = lane & 3;  // transposed roles: voxel (of 16), 8-channel group
   auto prefetch = [&](const RTile& tl, int dz) __attribute__((always_inline)) {
     if constexpr (PREF) {
@@ -423,15 +460,26 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     }
     uint4 ax[2][RMS + 2];
     uint4 bw[2][3];
-    auto load_a = [&](uint4* af, int kw) __attribute__((always_inline)) {
+    if constexpr ((ROLL_ABL & 8) != 0) {
 #pragma unroll
-      for (int hr = 0; hr < RMS + 2; ++hr) af[hr] = *reinterpret_cast<const uint4*>(sl + abase[kw] + hr * RHW * 32);
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int j = 0; j < RMS + 2; ++j) ax[i][j] = make_uint4(lane, 1, 2, 3);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) bw[i][j] = make_uint4(lane, 3, 2, 1);
+      }
+    }
+    auto load_a = [&](uint4* af, int kw) __attribute__((always_inline)) {
+      if constexpr (!(ROLL_ABL & 8))
+#pragma unroll
+        for (int hr = 0; hr < RMS + 2; ++hr) af[hr] = *reinterpret_cast<const uint4*>(sl + abase[kw] + hr * RHW * 32);
     };
     auto load_b = [&](uint4* bf, int g) __attribute__((always_inline)) {
       const int kw = g / NACC, b = g % NACC;
       const char* pb = sl + bbase + bofs[b] + kw * NT * 1024;
+      if constexpr (!(ROLL_ABL & 8))
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh) bf[kh] = *reinterpret_cast<const uint4*>(pb + kh * 3 * NT * 1024);
+        for (int kh = 0; kh < 3; ++kh) bf[kh] = *reinterpret_cast<const uint4*>(pb + kh * 3 * NT * 1024);
     };
     load_a(ax[0], 0);
     load_b(bw[0], 0);
@@ -440,10 +488,10 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       const int kw = g / NACC, b = g % NACC;
       if (g + 1 < G::NG) load_b(bw[(g + 1) & 1], g + 1);
       if (b == (NACC == 3 ? 1 : 0) && kw + 1 < 3) load_a(ax[(kw + 1) & 1], kw + 1);
-      if (g < RNQ && don) dma(dn, g, (SLOT + 2) % 3);
+      if (g < RNQ && (ROLL_LEAN || don)) dma(dn, g, (SLOT + 2) % 3);
       if constexpr (PRO) {
         if (g == RNQ && tnext) {
-          if (don) roll_wait_vmcnt<RNQ>();  // the next stage's pieces landed (the one after stays in flight)
+          if (ROLL_LEAN || don) roll_wait_vmcnt<RNQ>();  // the next stage's pieces landed (the one after stays in flight)
           else roll_wait_vmcnt<0>();
         }
         if (g >= RNQ && tnext) {
@@ -457,7 +505,8 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
         for (int kh = 0; kh < 3; ++kh) {
           if (SP == SP_NONE || ((tkb >> (kh * 3 + kw)) & 1)) {
 #pragma unroll
-            for (int ms = 0; ms < RMS; ++ms) mma<H>(acc[b][ms], bw[g & 1][kh], ax[kw & 1][ms + kh]);
+            for (int ms = 0; ms < RMS; ++ms)
+              if constexpr (!(ROLL_ABL & 1)) mma<H>(acc[b][ms], bw[g & 1][kh], ax[kw & 1][ms + kh]);
           }
         }
       }
@@ -514,8 +563,16 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
           if constexpr (EM & RE_BNRED) {
             float tr[8], xb[8];
             Chunk<H>::unpack(Chunk<H>::pack(t), tr);  // the stored (rounded) dz, as the separate reduce reads it
-            Chunk<H>::unpack(*reinterpret_cast<const uint4*>(reinterpret_cast<const H*>(a.bnx) +
-                                                             (yp - reinterpret_cast<H*>(a.y.ptr))), xb);
+            uint4 xv;
+            if constexpr (PREF) {
+              if (use_pre) xv = __builtin_bit_cast(uint4, pre[ms][nt][k]);
+              else xv = *reinterpret_cast<const uint4*>(reinterpret_cast<const H*>(a.bnx) +
+                                                        (yp - reinterpret_cast<H*>(a.y.ptr)));
+            } else {
+              xv = *reinterpret_cast<const uint4*>(reinterpret_cast<const H*>(a.bnx) +
+                                                   (yp - reinterpret_cast<H*>(a.y.ptr)));
+            }
+            Chunk<H>::unpack(xv, xb);
             float cst[4][8];  // scale, shift, mean, invstd of the lane's 8 channels
 #pragma unroll
             for (int k4 = 0; k4 < 4; ++k4) {
@@ -600,7 +657,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       for (int b = 0; b < 3; ++b) {
         if (all || b == bdone) {
           const int dz = P - (P + 3 - b) % 3;  // the output depth in bank b
-          if (dz >= tl.z0 && dz < tl.z1) epilogue_tr(acc[b], tl, dz, 0, false, scr);
+          if (!(ROLL_ABL & 4) && dz >= tl.z0 && dz < tl.z1) epilogue_tr(acc[b], tl, dz, 0, use_pre && b == bdone, scr);
 #pragma unroll
           for (int m = 0; m < RMS; ++m)
 #pragma unroll
@@ -634,7 +691,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     } else {
 #pragma unroll
       for (int b = 0; b < NACC; ++b) {
-        if (P >= tl.z0 && P < tl.z1) epilogue_tr(acc[b], tl, P, b, use_pre, scr);
+        if (!(ROLL_ABL & 4) && P >= tl.z0 && P < tl.z1) epilogue_tr(acc[b], tl, P, b, use_pre, scr);
 #pragma unroll
         for (int m = 0; m < RMS; ++m)
 #pragma unroll
@@ -668,6 +725,13 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
 #pragma unroll
     for (int q = 0; q < RNQ; ++q) dma(d1, q, 1);
     vn = advance(nx);
+  } else if constexpr (ROLL_LEAN) {  // zero-page pieces: the waits below count two batches
+    Dma d1;
+    d1.xb = nullptr;
+    d1.wsrc = nullptr;
+    d1.use = 0;
+#pragma unroll
+    for (int q = 0; q < RNQ; ++q) dma(d1, q, 1);
   }
   // the stage after the current one, for the late prologue: exists, chunk, lane mask
   bool tnext;
@@ -682,7 +746,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   }
   __syncthreads();  // bias / prologue tables visible
   if constexpr (PRO) {  // the first stage: no earlier compute transformed it
-    if (tnext) roll_wait_vmcnt<RNQ>();
+    if (ROLL_LEAN || tnext) roll_wait_vmcnt<RNQ>();
     else roll_wait_vmcnt<0>();
 #pragma unroll
     for (int q = 0; q < RNA; ++q) transform_piece(lds, q, 0, cm);
@@ -706,24 +770,27 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     fscr = lds + ((decltype(slot_c)::value + 2) % 3) * RSLOT;
     if (PREF && pf_hold > 0) {
       --pf_hold;
-      if (tnext) roll_wait_vmcnt<RNQ + NPF>();  // this stage landed; the next stage and the prefetch stay in flight
+      if (ROLL_LEAN || tnext) roll_wait_vmcnt<RNQ + NPF>();  // this stage landed; the next stage and the prefetch stay in flight
       else roll_wait_vmcnt<NPF>();
     } else {
-      if (tnext) roll_wait_vmcnt<RNQ>();  // this stage landed (and any earlier prefetch); the next stays in flight
+      if (ROLL_LEAN || tnext) roll_wait_vmcnt<RNQ>();  // this stage landed (and any earlier prefetch); the next stays in flight
       else roll_wait_vmcnt<0>();
     }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // this slot ready, the previous one free
+    if constexpr (ROLL_ABL & 16) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // this slot ready, the previous one free
     if (pdi >= 0) {
       if (ppre) settle();
       flush(ptl, pdi, pall, ppre, lds + ((decltype(slot_c)::value + 2) % 3) * RSLOT);
     }
     const int di = ct.di_lo + cs;
-    const bool out_in = di + a.pd >= ct.z0 && di + a.pd < ct.z1;  // this slice completes an output depth (2-D)
+    // the output depth this slice completes: 2-D di + pd, 3-D the bank of di + pd - 2
+    const int pz = KD == 3 ? di + a.pd - 2 : di + a.pd;
+    const bool out_in = pz >= ct.z0 && pz < ct.z1;
     bool pf_next = false;
     if constexpr (PREF) {
       if (a.nchunk == 1) {
         if (out_in) {
-          prefetch(ct, di + a.pd);
+          prefetch(ct, pz);
           pf_slice = true;
         }
       } else if (cc == max(a.nchunk - 3, 0) && out_in) {
@@ -744,7 +811,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     compute(slot_c, di + a.pd, kd_mask(ct.z0, ct.z1, di), dn, vn, tnext, tc, tm, tk0, tk1);
     if constexpr (PREF) {
       if (pf_next) {
-        prefetch(ct, di + a.pd);
+        prefetch(ct, pz);
         pf_slice = true;
         pf_hold = min(2, a.nchunk - 1);
       }
@@ -1058,6 +1125,7 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   if (bnred) {
     if (bnred->ws_floats < (size_t)ntiles * RNW * 64) return 0;
     a.bnx = (const char*)bnred->bnx->ptr;
+    a.msk = rview(bnred->bnx);  // the epilogue operand prefetch reads the BN input through msk
     a.bn_sc = bnred->scale;
     a.bn_sh = bnred->shift;
     a.bn_mu = bnred->mean;

@@ -27,12 +27,21 @@ epilogue):
   * Backward is hand-written (frames in reverse): every PReLU output's
     gradient is accumulated from all its consumers into the matching slice of
     a gradient buffer of the concat layout, then one fused pass applies the
-    PReLU derivative and reduces its slope gradient; conv weight gradients of
-    the weights shared by all frames accumulate across frames.
+    PReLU derivative and reduces its slope gradient.
+  * Weight gradients over the whole sequence at once: the weights are shared
+    by all T frames (drf_net.py:38-49), so every conv's weight gradient is
+    one launch over the B*T samples after the recurrent backward, instead of
+    T per-frame launches of B samples and T split-reduces (VSR_DRF_SEQ_WGRAD=0
+    keeps the per-frame launches on the side stream).  For that, every
+    operand a weight gradient reads -- forward activations and backward
+    output gradients -- is frame t of a (B, T, h, w, C) sequence buffer, so
+    frames 0..T-1 form one strided view (depth = frame: a kd = 1 conv treats
+    depth as batch).
 """
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -120,8 +129,24 @@ class _OutBlock(nn.Sequential):
         self.add_module(f"conv{len(steps) + 1}", nn.Conv2d(in_channels, out_channels, kernel_size=3, padding=1))
 
 
+def _seq_view(views: list) -> torch.Tensor | None:
+    """Frames 0..T-1 of one sequence buffer as a single (B, T, h, w, C) view,
+    given the per-frame (B, 1, h, w, C) views in frame order; None when they
+    are not evenly spaced slices of one buffer."""
+    v0 = views[0]
+    sd = v0.stride(1)
+    es = v0.element_size()
+    for t, v in enumerate(views):
+        if v.shape != v0.shape or v.stride() != v0.stride() or v.data_ptr() != v0.data_ptr() + t * sd * es:
+            return None
+    b, _, h, w, c = v0.shape
+    return torch.as_strided(v0, (b, len(views), h, w, c), v0.stride(), v0.storage_offset())
+
+
 class _DRFBase(BaseNet):
     _OVERLAP_WGRAD = True  # per-frame launches leave CUs idle: weight gradients fill them
+    # weight gradients batched over the sequence (see the module docstring)
+    SEQ_WGRAD = os.environ.get("VSR_DRF_SEQ_WGRAD", "1") != "0"
     def __init__(self, in_channels, out_channels, num_features, num_groups, upscale_factor):
         super().__init__()
         self.in_channels = in_channels
@@ -188,27 +213,43 @@ class _DRFBase(BaseNet):
         def new(hh, ww, c):
             return torch.empty((b, 1, hh, ww, c), dtype=cd, device=dev)
 
+        # training (tape): every tensor a weight gradient reads is frame t of
+        # a sequence buffer (B, T[+1], h, w, C); inference: per-frame buffers
+        T = len(frames)
+        seqs: dict | None = {} if tape is not None else None
+
+        def buf(name, t, hh, ww, c, nfr=T):
+            if seqs is None:
+                return new(hh, ww, c)
+            big = seqs.get(name)
+            if big is None:
+                big = seqs[name] = torch.empty((b, nfr, hh, ww, c), dtype=cd, device=dev)
+            return big[:, t:t + 1]
+
+        XV = None
+        if seqs is not None:  # all input frames in one layout move
+            XV = F.to_view(torch.stack([x.float() for x in frames], dim=2), cd, cpad=8)[..., :cin]
         outs, recs = [], []
-        X0 = new(h, w, 2 * f)
+        X0 = buf("X0", 0, h, w, 2 * f, T + 1)
         for t, x in enumerate(frames):
-            xv = F.to_view(x, cd, cpad=8)[..., :cin]
-            u1 = new(h, w, 4 * f)
+            xv = XV[:, t:t + 1] if XV is not None else F.to_view(x, cd, cpad=8)[..., :cin]
+            u1 = buf("u1", t, h, w, 4 * f)
             F.conv(xv, pw(ib.conv1), u1, K3, P1, bias=ib.conv1.bias, act=PR, act_param=ib.prelu1.weight)
             F.conv(u1, pw(ib.conv2), X0[..., :f], K1, P0, bias=ib.conv2.bias, act=PR, act_param=ib.prelu2.weight)
             if t == 0:  # hidden_state = in_features (drf_net.py:42-43)
                 F.conv(u1, pw(ib.conv2), X0[..., f:], K1, P0, bias=ib.conv2.bias, act=PR,
                        act_param=ib.prelu2.weight)
-            L = new(h, w, (G + 1) * f)
+            L = buf("L", t, h, w, (G + 1) * f)
             F.conv(X0, pw(fb.in_block.conv), L[..., :f], K1, P0, bias=fb.in_block.conv.bias, act=PR,
                    act_param=fb.in_block.prelu.weight)
-            Hc = new(H, W, G * f)
+            Hc = buf("Hc", t, H, W, G * f)
             t1s, t2s = [None] * G, [None] * G
             for i in range(G):
                 up, dn = fb.up_blocks[i], fb.down_blocks[i]
                 if i == 0:
                     src, dec, dpr = L[..., :f], up.deconv, up.prelu
                 else:
-                    src = new(h, w, f)
+                    src = buf(f"t1_{i}", t, h, w, f)
                     F.conv(L[..., :(i + 1) * f], pw(up.conv1), src, K1, P0, bias=up.conv1.bias, act=PR,
                            act_param=up.prelu1.weight)
                     t1s[i], dec, dpr = src, up.deconv2, up.prelu2
@@ -218,21 +259,21 @@ class _DRFBase(BaseNet):
                 if i == 0:
                     hsrc, cv, cpr = Hc[..., :f], dn.conv, dn.prelu
                 else:
-                    hsrc = new(H, W, f)
+                    hsrc = buf(f"t2_{i}", t, H, W, f)
                     F.conv(Hc[..., :(i + 1) * f], pw(dn.conv1), hsrc, K1, P0, bias=dn.conv1.bias, act=PR,
                            act_param=dn.prelu1.weight)
                     t2s[i], cv, cpr = hsrc, dn.conv2, dn.prelu2
                 wq, bq = sp(cv, False)
                 F.conv(hsrc, wq, L[..., (i + 1) * f:(i + 2) * f], K3, P1, bias=bq, x_shuffle=s, act=PR,
                        act_param=cpr.weight, subpixel=F.subpixel_code(k, s, p, False, False))
-            X0n = new(h, w, 2 * f)
+            X0n = buf("X0", t + 1, h, w, 2 * f, T + 1)
             ffeat = X0n[..., f:]  # f_features = next frame's hidden state (drf_net.py:45)
             F.conv(L[..., f:], pw(fb.out_block.conv), ffeat, K1, P0, bias=fb.out_block.conv.bias, act=PR,
                    act_param=fb.out_block.prelu.weight)
-            feat = F.add(X0[..., :f], ffeat, new(h, w, f))  # global residual skip (drf_net.py:46)
+            feat = F.add(X0[..., :f], ffeat, buf("feat", t, h, w, f))  # global residual skip (drf_net.py:46)
             u, hh, ww, ups_in = feat, h, w, []
-            for conv, st in self._ups():
-                nxt = new(hh * st, ww * st, f)
+            for j, (conv, st) in enumerate(self._ups()):
+                nxt = buf(f"up{j}", t, hh * st, ww * st, f)
                 F.conv(u, pw(conv, perm_r=st), nxt, K3, P1, bias=conv.bias, y_shuffle=st)
                 ups_in.append(u)
                 u, hh, ww = nxt, hh * st, ww * st
@@ -271,6 +312,23 @@ class _DRFBase(BaseNet):
         def new(hh, ww, c):
             return torch.empty((b, 1, hh, ww, c), dtype=cd, device=dev)
 
+        T = len(recs)
+        seq = self.SEQ_WGRAD
+        seqs: dict = {}
+
+        def sbuf(name, t, hh, ww, c):
+            """frame t of a backward sequence buffer (an output gradient a
+            weight gradient reads); per-frame buffers without SEQ_WGRAD"""
+            if not seq:
+                return new(hh, ww, c)
+            big = seqs.get(name)
+            if big is None:
+                big = seqs[name] = torch.empty((b, T, hh, ww, c), dtype=cd, device=dev)
+            return big[:, t:t + 1]
+
+        # deferred weight gradients: key -> (launch(x, dy, accumulate), {frame: (x, dy)})
+        pend: dict = {}
+
         def gbuf(prm):
             key = id(prm)
             if key in bufs:
@@ -279,58 +337,70 @@ class _DRFBase(BaseNet):
             bufs[key] = (prm, g)
             return g, False
 
-        def wgrad(conv, x, dy, ksz, pad, **kw):
+        def defer(key, t, x, dy, launch, acc):
+            """per frame: launch now (acc: accumulate onto the frames done so
+            far); SEQ_WGRAD: record frame t's operands, launched once over
+            the sequence"""
+            if not seq:
+                self._on_wgrad_stream(lambda: launch(x, dy, acc), x, dy)
+                return
+            pend.setdefault(id(key), (key, launch, {}))[2][t] = (x, dy)
+
+        def wgrad(conv, x, dy, ksz, pad, t, **kw):
             dw, acc = gbuf(conv.weight)
             db, _ = gbuf(conv.bias)
-            self._on_wgrad_stream(
-                lambda: F.conv_wgrad(x, dy, ksz, pad, dw.view(*dw.shape[:2], 1, *dw.shape[2:]), db, accumulate=acc,
-                                     **kw), x, dy)
+            defer(conv.weight, t, x, dy,
+                  lambda x_, dy_, acc_: F.conv_wgrad(x_, dy_, ksz, pad, dw.view(*dw.shape[:2], 1, *dw.shape[2:]), db,
+                                                     accumulate=acc_, **kw), acc)
 
-        def sp_wgrad(conv, x, dy, transposed):
+        def sp_wgrad(conv, x, dy, transposed, t):
             k_, s_, p_ = k, s, p
             cop = s_ * s_ * f if transposed else f
             cip = f if transposed else s_ * s_ * f
             dw, acc = gbuf(conv.weight)
             db, _ = gbuf(conv.bias)
 
-            def run():  # on the side stream: the sub-pixel wgrad and its fold
+            def run(x_, dy_, acc_):  # the sub-pixel wgrad and its fold
                 dweq = torch.empty((cop, cip, 1, 3, 3), dtype=torch.float32, device=dev)
                 dbeq = torch.empty(cop, dtype=torch.float32, device=dev)
                 spc = F.subpixel_code(k_, s_, p_, transposed, False)
                 if transposed:
-                    F.conv_wgrad(x, dy, K3, P1, dweq, dbeq, dy_shuffle=s_, subpixel=spc)
+                    F.conv_wgrad(x_, dy_, K3, P1, dweq, dbeq, dy_shuffle=s_, subpixel=spc)
                 else:
-                    F.conv_wgrad(x, dy, K3, P1, dweq, dbeq, x_shuffle=s_, subpixel=spc)
-                F.subpixel_wgrad_fold(dweq, dbeq, dw, db, k_, s_, p_, transposed, accumulate=acc)
+                    F.conv_wgrad(x_, dy_, K3, P1, dweq, dbeq, x_shuffle=s_, subpixel=spc)
+                F.subpixel_wgrad_fold(dweq, dbeq, dw, db, k_, s_, p_, transposed, accumulate=acc_)
 
-            self._on_wgrad_stream(run, x, dy)
+            defer(conv.weight, t, x, dy, run, acc)
 
         def prelu(y, dy, pr, out, dy2=None):
             da, acc = gbuf(pr.weight)
             return F.prelu_bwd(y, dy, pr.weight, out, da, acc, dy2=dy2)
 
+        co = self.out_channels
+        HH, WW = recs[0]["tail_in"].shape[2], recs[0]["tail_in"].shape[3]
+        gfull = [gys[t] if t < len(gys) and gys[t] is not None else
+                 torch.zeros((b, co, HH, WW), dtype=torch.float32, device=dev) for t in range(T)]
+        GV = F.to_view(torch.stack([g_.float() for g_ in gfull], dim=2), cd, cpad=8)[..., :co]  # (b, T, HH, WW, co)
         d_hidden = None  # grad of the previous frame's f_features (X0_t[..., f:])
-        for t in range(len(recs) - 1, -1, -1):
+        for t in range(T - 1, -1, -1):
             rc = recs[t]
-            gy = gys[t] if t < len(gys) and gys[t] is not None else None
             u = rc["tail_in"]
             hh, ww = u.shape[2], u.shape[3]
-            co = self.out_channels
-            if gy is None:
-                gy = torch.zeros((b, co, hh, ww), dtype=torch.float32, device=dev)
-            g = F.to_view(gy, cd, cpad=8)[..., :co]
+            g = GV[:, t:t + 1]
             tc = self._last_conv()
-            wgrad(tc, u, g, K3, P1)
-            du = F.conv(g, pw(tc, 1), new(hh, ww, f), K3, P1)
-            for (conv, st), uin in reversed(list(zip(self._ups(), rc["ups_in"]))):
-                wgrad(conv, uin, du, K3, P1, perm_r=st, dy_shuffle=st)
+            wgrad(tc, u, g, K3, P1, t)
+            ups = list(zip(self._ups(), rc["ups_in"]))
+            du = F.conv(g, pw(tc, 1), sbuf(f"du{len(ups)}", t, hh, ww, f), K3, P1)
+            for j in range(len(ups) - 1, -1, -1):
+                (conv, st), uin = ups[j]
+                wgrad(conv, uin, du, K3, P1, t, perm_r=st, dy_shuffle=st)
                 hh, ww = hh // st, ww // st
-                du = F.conv(du, pw(conv, 1, perm_r=st), new(hh, ww, f), K3, P1, x_shuffle=st)
+                du = F.conv(du, pw(conv, 1, perm_r=st), sbuf(f"du{j}", t, hh, ww, f), K3, P1, x_shuffle=st)
             gfeat = du  # grad of features = in_features + f_features
             L, Hc, X0 = rc["L"], rc["Hc"], rc["X0"]
             # f_block out: f_features feeds the skip and the next frame's hidden state
-            gout = prelu(rc["ffeat"], gfeat, fb.out_block.prelu, new(h, w, f), dy2=d_hidden)
-            wgrad(fb.out_block.conv, L[..., f:], gout, K1, P0)
+            gout = prelu(rc["ffeat"], gfeat, fb.out_block.prelu, sbuf("gout", t, h, w, f), dy2=d_hidden)
+            wgrad(fb.out_block.conv, L[..., f:], gout, K1, P0, t)
             # Concat gradients without zero fills (the high-res one is 0.5 GB
             # per frame at cfg 3): the first contributor to a slice writes it,
             # later ones accumulate.  dL[..., f:] is first written by the
@@ -346,54 +416,63 @@ class _DRFBase(BaseNet):
                 # down projection -> lr_{i+1} = L[..., (i+1)f:(i+2)f]
                 cv, cpr = (dn.conv, dn.prelu) if i == 0 else (dn.conv2, dn.prelu2)
                 sl = slice((i + 1) * f, (i + 2) * f)
-                gl = prelu(L[..., sl], dL[..., sl], cpr, new(h, w, f))
+                gl = prelu(L[..., sl], dL[..., sl], cpr, sbuf(f"gl{i}", t, h, w, f))
                 hsrc = Hc[..., :f] if i == 0 else rc["t2s"][i]
-                sp_wgrad(cv, hsrc, gl, transposed=False)
+                sp_wgrad(cv, hsrc, gl, False, t)
                 wq1, _ = sp(cv, False, 1)
                 spc = F.subpixel_code(k, s, p, False, True)
                 if i == 0:
                     F.conv(gl, wq1, dHc[..., :f], K3, P1, y_shuffle=s, accumulate=G > 1, subpixel=spc)
                 else:
-                    dt2 = new(H, W, f)
+                    dt2 = sbuf(f"dt2_{i}", t, H, W, f)
                     da, acc = gbuf(dn.prelu1.weight)
                     if not F.conv_prelu_bwd(gl, wq1, dt2, K3, P1, rc["t2s"][i], dn.prelu1.weight, da, acc,
                                             y_shuffle=s, subpixel=spc):
                         F.conv(gl, wq1, dt2, K3, P1, y_shuffle=s, subpixel=spc)
                         F.prelu_bwd(rc["t2s"][i], dt2, dn.prelu1.weight, dt2, da, acc)
-                    wgrad(dn.conv1, Hc[..., :(i + 1) * f], dt2, K1, P0)
+                    wgrad(dn.conv1, Hc[..., :(i + 1) * f], dt2, K1, P0, t)
                     F.conv(dt2, pw(dn.conv1, 1), dHc[..., :(i + 1) * f], K1, P0, accumulate=i != G - 1)
                 # up projection -> hr_i = Hc[..., i f:(i+1) f]
                 dec, dpr = (up.deconv, up.prelu) if i == 0 else (up.deconv2, up.prelu2)
                 sh = slice(i * f, (i + 1) * f)
-                gh = prelu(Hc[..., sh], dHc[..., sh], dpr, new(H, W, f))
+                gh = prelu(Hc[..., sh], dHc[..., sh], dpr, sbuf(f"gh{i}", t, H, W, f))
                 src = L[..., :f] if i == 0 else rc["t1s"][i]
-                sp_wgrad(dec, src, gh, transposed=True)
+                sp_wgrad(dec, src, gh, True, t)
                 wq1, _ = sp(dec, True, 1)
                 spc = F.subpixel_code(k, s, p, True, True)
                 if i == 0:
                     F.conv(gh, wq1, dL[..., :f], K3, P1, x_shuffle=s, accumulate=True, subpixel=spc)
                 else:
-                    dt1 = new(h, w, f)
+                    dt1 = sbuf(f"dt1_{i}", t, h, w, f)
                     da, acc = gbuf(up.prelu1.weight)
                     if not F.conv_prelu_bwd(gh, wq1, dt1, K3, P1, rc["t1s"][i], up.prelu1.weight, da, acc,
                                             x_shuffle=s, subpixel=spc):
                         F.conv(gh, wq1, dt1, K3, P1, x_shuffle=s, subpixel=spc)
                         F.prelu_bwd(rc["t1s"][i], dt1, up.prelu1.weight, dt1, da, acc)
-                    wgrad(up.conv1, L[..., :(i + 1) * f], dt1, K1, P0)
+                    wgrad(up.conv1, L[..., :(i + 1) * f], dt1, K1, P0, t)
                     F.conv(dt1, pw(up.conv1, 1), dL[..., :(i + 1) * f], K1, P0, accumulate=True)
-            g0 = prelu(L[..., :f], dL[..., :f], fb.in_block.prelu, new(h, w, f))
-            wgrad(fb.in_block.conv, X0, g0, K1, P0)
+            g0 = prelu(L[..., :f], dL[..., :f], fb.in_block.prelu, sbuf("g0", t, h, w, f))
+            wgrad(fb.in_block.conv, X0, g0, K1, P0, t)
             dX0 = F.conv(g0, pw(fb.in_block.conv, 1), new(h, w, 2 * f), K1, P0)
             if t == 0:  # the first hidden state is in_features itself
                 F.add(dX0[..., :f], dX0[..., f:], dX0[..., :f])
                 d_hidden = None
             else:
                 d_hidden = dX0[..., f:]
-            gin = prelu(X0[..., :f], gfeat, ib.prelu2, new(h, w, f), dy2=dX0[..., :f])
-            wgrad(ib.conv2, rc["u1"], gin, K1, P0)
-            du1 = F.conv(gin, pw(ib.conv2, 1), new(h, w, 4 * f), K1, P0)
+            gin = prelu(X0[..., :f], gfeat, ib.prelu2, sbuf("gin", t, h, w, f), dy2=dX0[..., :f])
+            wgrad(ib.conv2, rc["u1"], gin, K1, P0, t)
+            du1 = F.conv(gin, pw(ib.conv2, 1), sbuf("du1", t, h, w, 4 * f), K1, P0)
             prelu(rc["u1"], du1, ib.prelu1, du1)
-            wgrad(ib.conv1, rc["xv"], du1, K3, P1)
+            wgrad(ib.conv1, rc["xv"], du1, K3, P1, t)
+        # every shared weight's gradient once over the sequence (frames as depth)
+        for key, launch, frs in pend.values():
+            xs = _seq_view([frs[t][0] for t in range(T)])
+            dys = _seq_view([frs[t][1] for t in range(T)])
+            if xs is not None and dys is not None:
+                launch(xs, dys, False)
+            else:  # operands not in sequence buffers: per frame, accumulated
+                for t in range(T):
+                    launch(frs[t][0], frs[t][1], t > 0)
         for prm, g in bufs.values():
             self._grad_done(grads, prm, g)
         return grads
