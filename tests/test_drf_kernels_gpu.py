@@ -164,3 +164,25 @@ def test_prelu_epilogue_and_backward(dtype):
     gin = Fn.conv_transpose2d(_nchw(_q(gz, dtype)), _q(wt, dtype), padding=1)
     refm = _cl(torch.where(_nchw(y.double().cpu()) > 0, gin, 0.2 * gin))
     assert (d_in.double().cpu() - refm).abs().max().item() <= _tol(dtype, refm) * 2
+
+
+@pytest.mark.parametrize("slope", [0.0, -0.3])
+def test_prelu_slope_gradient_nonpositive_slope_is_loud(slope):
+    """The tape keeps PReLU outputs only; y < 0 marks x < 0 only while a > 0.
+    With a <= 0 both slope-gradient paths (prelu_bwd and the fused rolling
+    dgrad, vsrk_conv_fwd_prelu_bwd) write NaN instead of a silently wrong
+    value."""
+    g = torch.Generator().manual_seed(5)
+    dt = torch.bfloat16
+    n, h, w, f = 1, 8, 16, 64
+    y = torch.randn((n, 1, h, w, f), generator=g).to(DEV, dt)
+    gy = torch.randn((n, 1, h, w, f), generator=g).to(DEV, dt)
+    ad = torch.tensor([slope], device=DEV)
+    da = torch.zeros(1, device=DEV)
+    F.prelu_bwd(y, gy, ad, torch.empty_like(y), da, accumulate_da=False)
+    assert torch.isnan(da).all()
+    wt = torch.randn((f, f, 3, 3), generator=g).to(DEV) / 24
+    da2 = torch.zeros(1, device=DEV)
+    ran = F.conv_prelu_bwd(gy, F.pack_weight(wt, 1, dt), torch.empty_like(y), (1, 3, 3), (0, 1, 1), y, ad, da2, False)
+    if ran:
+        assert torch.isnan(da2).all()

@@ -241,7 +241,11 @@ def build_test(config, device=None):
     test_dataset = build_dataset(config.dataset, 'test')
     dl = Box(config.dataloader.to_dict())
     dl.kwargs = dl.get('kwargs') or Box()
-    dl.kwargs.update(shard_padding=False)
+    # the test set is never sharded: under torchrun every rank would otherwise
+    # write the same results.csv / PNGs / GIFs from its own shard, and a
+    # sequence could straddle two shards; each rank runs the whole set and
+    # only rank 0 exports (BasePredictor.predict)
+    dl.kwargs.update(shard_padding=False, distributed=False)
     test_loader = get_instance(ns['data'], dl, test_dataset)
     net = build_net(config)
     loss_fns, loss_weights = build_losses(config)

@@ -931,7 +931,11 @@ __global__ __launch_bounds__(1024) void roll_slope_final_kernel(const float* __r
   }
   if (threadIdx.x == 0) {
     const double av = (double)*a;
-    const float v = (float)(sh[0] / (av * av));
+    // The tape holds PReLU outputs only: y < 0 marks x < 0 only while a > 0.
+    // A slope <= 0 makes the output-based gradient ambiguous, so it poisons
+    // da with NaN (a loud failure in the optimizer step, never a silently
+    // wrong gradient); nn.PReLU starts at 0.2 (drf_net.py:56).
+    const float v = av > 0.0 ? (float)(sh[0] / (av * av)) : __builtin_nanf("");
     *da = accumulate ? *da + v : v;
   }
 }

@@ -390,12 +390,12 @@ class _DRFBase(BaseNet):
             tc = self._last_conv()
             wgrad(tc, u, g, K3, P1, t)
             ups = list(zip(self._ups(), rc["ups_in"]))
-            du = F.conv(g, pw(tc, 1), sbuf(f"du{len(ups)}", t, hh, ww, f), K3, P1)
+            du = F.conv(g, pw(tc, 1), sbuf(f"dup{len(ups)}", t, hh, ww, f), K3, P1)
             for j in range(len(ups) - 1, -1, -1):
                 (conv, st), uin = ups[j]
                 wgrad(conv, uin, du, K3, P1, t, perm_r=st, dy_shuffle=st)
                 hh, ww = hh // st, ww // st
-                du = F.conv(du, pw(conv, 1, perm_r=st), sbuf(f"du{j}", t, hh, ww, f), K3, P1, x_shuffle=st)
+                du = F.conv(du, pw(conv, 1, perm_r=st), sbuf(f"dup{j}", t, hh, ww, f), K3, P1, x_shuffle=st)
             gfeat = du  # grad of features = in_features + f_features
             L, Hc, X0 = rc["L"], rc["Hc"], rc["X0"]
             # f_block out: f_features feeds the skip and the next frame's hidden state
@@ -461,7 +461,7 @@ class _DRFBase(BaseNet):
                 d_hidden = dX0[..., f:]
             gin = prelu(X0[..., :f], gfeat, ib.prelu2, sbuf("gin", t, h, w, f), dy2=dX0[..., :f])
             wgrad(ib.conv2, rc["u1"], gin, K1, P0, t)
-            du1 = F.conv(gin, pw(ib.conv2, 1), sbuf("du1", t, h, w, 4 * f), K1, P0)
+            du1 = F.conv(gin, pw(ib.conv2, 1), sbuf("du_u1", t, h, w, 4 * f), K1, P0)
             prelu(rc["u1"], du1, ib.prelu1, du1)
             wgrad(ib.conv1, rc["xv"], du1, K3, P1, t)
         # every shared weight's gradient once over the sequence (frames as depth)

@@ -32,6 +32,7 @@ from pathlib import Path
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from .. import metrics as M
 from ..callbacks.monitor import safe_globals
@@ -174,6 +175,9 @@ class BasePredictor:
 
     def predict(self):
         self.net.eval()
+        # data-parallel launch (torchrun): the test loader is unsharded
+        # (vsr_amd.config.build_test) and only rank 0 writes the exports
+        exported = self.exported and not (dist.is_available() and dist.is_initialized() and dist.get_rank() != 0)
         header = (["name"] + [fn.__class__.__name__ for fn in self.metric_fns] +
                   [fn.__class__.__name__ for fn in self.loss_fns])
         results = [header]
@@ -191,7 +195,7 @@ class BasePredictor:
                 loss = (losses.mean(dim=0) * self.loss_weights).sum()
                 metrics = self._frame_metrics(outs, tgts, patient)      # (T, M)
             T = len(outs)
-            if self.exported:
+            if exported:
                 self._export(state, results, filename, patient, sid, fid, outs, metrics, losses)
             # acdc_vsr_predictor.py:160-170: frame-weighted
             log["Loss"] += loss.item() * T
@@ -200,7 +204,7 @@ class BasePredictor:
             for fn, v in zip(self.metric_fns, metrics.mean(dim=0)):
                 log[fn.__class__.__name__] += v.item() * T
             count += T
-        if self.exported:
+        if exported:
             self._flush_video(state)
             self.saved_dir.mkdir(parents=True, exist_ok=True)
             with open(self.saved_dir / "results.csv", "w", newline="") as fh:
