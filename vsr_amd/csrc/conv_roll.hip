@@ -70,6 +70,16 @@ constexpr int RNSLOT = 3;
 #ifndef ROLL_LEAN
 #define ROLL_LEAN 1
 #endif
+// ROLL_PFASM (default 0): the epilogue operand prefetch as inline-asm loads
+// the compiler cannot see.  Their destination registers then look ready at
+// once, so nothing stops the register allocator from copying or re-using
+// them before the data lands (round 4: a restructured epilogue read stale
+// residual / mask operands).  Default: ordinary loads, which the compiler
+// waits for before their first use -- at the flush, where that wait may
+// also drain the next stage's pieces (issued a stage earlier).
+#ifndef ROLL_PFASM
+#define ROLL_PFASM 0
+#endif
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
@@ -89,13 +99,24 @@ __device__ __forceinline__ void glds16_m0(const void* gsrc, uint32_t lds_base) {
 // Conv 3x3 over depth-1 slices (a Conv2d on a D = 1 view), two 32-channel
 // output blocks sharing every A fragment (the 64-channel EDSR body convs).
 // B piece p = tap * NT + nt holds (tap, output block nt): 32 channels x 32 B.
-template <int KD, int NT>
+// WR (resident weights): the whole weight image of the output block -- every
+// input chunk's B pieces, nchunk x NB KB -- is loaded into LDS once (per
+// workgroup, or when the walk enters another output block) instead of riding
+// in every stage's slot.  The LDS-DMA issue of a piece costs ~60-185 cycles
+// beside MFMAs (MI355X_MICROARCH.md) and the ablations of this kernel showed
+// the DMA pieces at about a third of its time: a stage then brings the 20 A
+// pieces only (EDSR body 64 -> 64: 38 -> 20 pieces; DUF data gradient
+// 32 -> F: 47 -> 20).
+template <int KD, int NT, int WR = 0>
 struct RollGeo {
   static_assert((KD == 3 && NT == 1) || (KD == 1 && NT == 2), "rolling conv forms: 3x3x3 / 32 or 3x3 / 64");
   static constexpr int NB = 9 * KD * NT;           // B pieces: 27 / 18
-  static constexpr int NI = RNAI + NB;             // 47 / 38
-  static constexpr int NQ = (NI + RNW - 1) / RNW;  // pieces per wave and stage: 6 / 5
-  static constexpr int SLOT = NQ * RNW * 1024;     // 48 KB / 40 KB: A | B | junk pieces
+  static constexpr int NI = WR ? RNAI : RNAI + NB;  // 47 / 38 (WR: 20)
+  static constexpr int NQ = (NI + RNW - 1) / RNW;  // pieces per wave and stage: 6 / 5 (WR: 3)
+  // 48 KB / 40 KB: A | B | junk pieces.  WR: 24 KB (2-D: the transposed
+  // epilogue parks a row in two halves, 2 KB per wave) or 32 KB (3-D: room
+  // for the one-pass 4 KB park; the fourth piece per wave is never loaded)
+  static constexpr int SLOT = (WR && KD == 3 ? 4 : NQ) * RNW * 1024;
   static constexpr int NACC = KD * NT;             // accumulator sets: banks (KD 3) or blocks (KD 1)
   static constexpr int NG = 3 * NACC;              // compute groups (kw, set): 9 / 6
   static constexpr int NTG = NG - NQ;              // groups that carry the late prologue: 3 / 1
@@ -174,11 +195,19 @@ __device__ __forceinline__ void roll_wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int KD, int NT, int PRO, int EM, int SP, typename H>
+template <int KD, int NT, int PRO, int EM, int SP, typename H, int WR>
 __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   static_assert(SP == SP_NONE || KD == 1, "sub-pixel views: 2-D form only");
-  using G = RollGeo<KD, NT>;
+  static_assert(!WR || SP == SP_NONE, "resident weights: plain views only");
+  using G = RollGeo<KD, NT, WR>;
   constexpr int RNQ = G::NQ, RSLOT = G::SLOT, NACC = G::NACC;
+  // the transposed epilogue parks a row in two halves (2 KB of scratch per
+  // wave) where the slot is too small for one 4 KB park (WR)
+#ifdef ROLL_PARK2
+  constexpr bool PARK2 = ROLL_PARK2 || (WR && KD == 1);
+#else
+  constexpr bool PARK2 = WR && KD == 1;
+#endif
   // the residual / mask operand of a 2-D tile is loaded into registers during
   // its last stage (one extra operand, no accumulate)
   // (3-D: the BN input of RE_BNRED, read by the flush of the slice's finished depth)
@@ -188,7 +217,8 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  float* lbias = reinterpret_cast<float*>(lds + RNSLOT * RSLOT);  // [cout_pad] bias * out_scale
+  char* wres = lds + RNSLOT * RSLOT;  // WR: [chunk][B piece] 1 KB pieces of the resident output block
+  float* lbias = reinterpret_cast<float*>(wres + (WR ? a.nchunk * G::NB * 1024 : 0));  // [cout_pad] bias * out_scale
   float* lsc = lbias + a.cout_pad;                                // [cin_pad] prologue scale / shift
   float* lsh = lsc + a.cin_pad;
   if constexpr (PRO) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, a.cin_pad, tid, RNW * 64);
@@ -264,7 +294,8 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
 #pragma unroll
   for (int kw = 0; kw < 3; ++kw)
     abase[kw] = (uint32_t)((wave * RMS * RHW + kw + r) * 32 + 16 * (hf ^ (((kw + r) >> 3) & 1)));
-  const uint32_t bbase = (uint32_t)(RNAI * 1024 + r * 32 + 16 * (hf ^ ((r >> 3) & 1)));
+  // (WR: the B pieces of the stage's chunk in the resident image, same piece layout)
+  const uint32_t bbase = (uint32_t)((WR ? 0 : RNAI * 1024) + r * 32 + 16 * (hf ^ ((r >> 3) & 1)));
 
   // ---- tiles of this workgroup (XCD group x owns a contiguous range) ----
   const int G_ = gridDim.x;
@@ -376,6 +407,24 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[k][m][i] = 0.f;
 
+  // WR: the whole weight image of output block n0 into the resident region
+  // (piece p = chunk * NB + (tap, nt); each wave issues every 8th piece)
+  int wblk = -1;  // output block held by the resident region
+  auto load_w = [&](int n0) __attribute__((always_inline)) {
+    if constexpr (WR) {
+      const int nw = a.nchunk * G::NB;
+      const int co = lane >> 1;
+      const int ph = (lane & 1) ^ ((co >> 3) & 1);
+      for (int p = wave; p < nw; p += RNW) {
+        const int c = p / G::NB, bp = p - c * G::NB;
+        const int tap = bp / NT, nt = bp - tap * NT;
+        const H* src = reinterpret_cast<const H*>(a.w) + ((tap * a.cout_pad + n0 + nt * 32 + co) * a.cin_pad + c * RCH + 8 * ph);
+        glds16_m0(src, lds_addr(wres) + p * 1024);
+      }
+      wblk = n0;
+    }
+  };
+
   // BN-affine/ReLU prologue on this lane's own landed A piece q of slot `sl`
   // (in-image pieces; the halo stays zero as in the reference, which pads
   // relu(bn(x))): c = the stage's channel chunk, m = its lane mask.
@@ -389,19 +438,21 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     }
   };
 
-  // Epilogue operand prefetch (2-D, one operand), in the transposed
-  // epilogue's layout: lane l reads 8 channels (16 bytes) 8 (l & 3) .. +7 of
-  // the block of voxel (l >> 2) + 16 k.  The loads are inline asm like the
-  // DMA pieces: the compiler's own vmcnt bookkeeping cannot see those, and
-  // would drain the in-flight stage at the first use.  The stage waits of the
-  // main loop retire them (see pf_hold); `settle` ties the uses after the
-  // flush's barrier.
+  // Epilogue operand prefetch (2-D: the residual or mask; 3-D: the BN input
+  // of RE_BNRED), in the transposed epilogue's layout: lane l reads 8
+  // channels (16 bytes) 8 (l & 3) .. +7 of the block of voxel (l >> 2) + 16 k,
+  // a slice's last stages ahead of its flush.  The stage waits of the main
+  // loop count them (see pf_hold) and retire them before the flush; as
+  // ordinary loads (ROLL_PFASM 0) the compiler also waits for them itself
+  // before their first use.
   typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
   u32x4_t pre[PREF ? RMS : 1][PREF ? NT : 1][2];
   const RView& pv = (EM & RE_RES) ? a.res : a.msk;  // (RE_BNRED: msk is the BN input view)
   const int tv = lane >> 2, tc8 = lane & 3;  // transposed roles: voxel (of 16), 8-channel group
   auto prefetch = [&](const RTile& tl, int dz) __attribute__((always_inline)) {
-    if constexpr (PREF) {
+    // (ablation 2 issues no DMA, so the compile-time waits would not cover
+    // these register loads: never combine them)
+    if constexpr (PREF && !(ROLL_ABL & 2)) {
 #pragma unroll
       for (int ms = 0; ms < RMS; ++ms) {
         const int ho = tl.h0 + wave * RMS + ms;
@@ -414,7 +465,10 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) {
             const void* src = ok ? (const void*)(pp + nt * 32) : (const void*)zp;
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(pre[ms][nt][k]) : "v"(src) : "memory");
+            if constexpr (ROLL_PFASM)
+              asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(pre[ms][nt][k]) : "v"(src) : "memory");
+            else
+              pre[ms][nt][k] = *reinterpret_cast<const u32x4_t*>(src);
           }
         }
       }
@@ -441,9 +495,10 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // this wave's A pieces of the NEXT stage (slot SLOT+1, landed one stage
   // ago), beside the MFMAs instead of in front of the barrier.
   auto compute = [&](auto slot_c, int P, unsigned km, const Dma& dn, bool don, bool tnext, int tc,
-                     unsigned tm, unsigned tk0, unsigned tk1) __attribute__((always_inline)) {
+                     unsigned tm, unsigned tk0, unsigned tk1, int cchunk) __attribute__((always_inline)) {
     constexpr int SLOT = decltype(slot_c)::value;
     const char* sl = lds + SLOT * RSLOT;
+    const char* bsl = WR ? wres + cchunk * G::NB * 1024 : sl;  // where this stage's B pieces are
     char* sl1 = lds + ((SLOT + 1) % 3) * RSLOT;
     const int pm = P % 3;
     uint32_t bofs[NACC];  // byte offset of set b's taps
@@ -476,7 +531,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     };
     auto load_b = [&](uint4* bf, int g) __attribute__((always_inline)) {
       const int kw = g / NACC, b = g % NACC;
-      const char* pb = sl + bbase + bofs[b] + kw * NT * 1024;
+      const char* pb = bsl + bbase + bofs[b] + kw * NT * 1024;
       if constexpr (!(ROLL_ABL & 8))
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh) bf[kh] = *reinterpret_cast<const uint4*>(pb + kh * 3 * NT * 1024);
@@ -525,10 +580,11 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // x 64 bytes -- instead of 32 voxels x 8 bytes, which doubled the cost of a
   // residual / mask operand in the 2-D form and of the BN input read in the
   // fused 3-D data gradient (2.0 vs 1.24 ms per DUF launch, round 3).
-  // The scratch is the wave's own DMA pieces 0-3 of the slot the next DMA
+  // The scratch is the wave's own DMA pieces 0-1 of the slot the next DMA
   // fills (free after the barrier; only this wave writes them, and only after
-  // its flush): voxel v in piece v / 8, row v % 8 (128 bytes), 16-byte column
-  // c at c ^ (v & 7) (conflict-free parking and read-back).
+  // its flush): a row is parked in two halves of 16 voxels, voxel v in piece
+  // (v % 16) / 8, row v % 8 (128 bytes), 16-byte column c at c ^ (v & 7)
+  // (conflict-free parking and read-back; 2 KB per wave fits every slot form).
   auto epilogue_tr = [&](const f32x16 (&A)[RMS], const RTile& tl, int dz, int nt, bool use_pre, char* scr)
                          __attribute__((always_inline)) {
     char* ws = scr + wave * 1024;
@@ -536,18 +592,26 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     for (int ms = 0; ms < RMS; ++ms) {
       const int ho = tl.h0 + wave * RMS + ms;
       if (ho >= a.y.h) continue;  // wave-uniform
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(ws + (r >> 3) * 8 * 1024 + (r & 7) * 128 + (((2 * g + hf) ^ (r & 7)) * 16)) =
-            make_float4(A[ms][4 * g], A[ms][4 * g + 1], A[ms][4 * g + 2], A[ms][4 * g + 3]);
       const int co = tl.n0 + nt * 32 + 8 * tc8;
       const float4 b0 = *reinterpret_cast<const float4*>(lbias + co);
       const float4 b1 = *reinterpret_cast<const float4*>(lbias + co + 4);
       const float bsv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      if constexpr (!PARK2) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(ws + (r >> 3) * 8 * 1024 + (r & 7) * 128 + (((2 * g + hf) ^ (r & 7)) * 16)) =
+              make_float4(A[ms][4 * g], A[ms][4 * g + 1], A[ms][4 * g + 2], A[ms][4 * g + 3]);
+      }
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
+        if (PARK2 && (r >> 4) == k) {  // this half's 16 voxels park their 32 channels
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(ws + ((r >> 3) & 1) * 8 * 1024 + (r & 7) * 128 + (((2 * g + hf) ^ (r & 7)) * 16)) =
+                make_float4(A[ms][4 * g], A[ms][4 * g + 1], A[ms][4 * g + 2], A[ms][4 * g + 3]);
+        }
         const int v = tv + 16 * k, wo = tl.w0 + v;
-        const char* rb = ws + (v >> 3) * 8 * 1024 + (v & 7) * 128;
+        const char* rb = PARK2 ? ws + (tv >> 3) * 8 * 1024 + (tv & 7) * 128 : ws + (v >> 3) * 8 * 1024 + (v & 7) * 128;
         const float4 q0 = *reinterpret_cast<const float4*>(rb + (((2 * tc8) ^ (v & 7)) * 16));
         const float4 q1 = *reinterpret_cast<const float4*>(rb + (((2 * tc8 + 1) ^ (v & 7)) * 16));
         float t[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
@@ -714,6 +778,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   RTile ct = nx.tl;
   unsigned cm = nx.m;
   int cs = 0, cc = 0;
+  load_w(ct.n0);  // WR: retired by the first stage's wait (it is older), visible after its barrier
   {
     const Dma d0 = prep(nx);
 #pragma unroll
@@ -778,9 +843,25 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     }
     if constexpr (ROLL_ABL & 16) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // this slot ready, the previous one free
+    // WR: the compute walk entered a tile of another output block.  Every
+    // wave is past the last stage that read the old image (the barrier
+    // above), so the new one is issued now, its latency covered by the flush,
+    // then drained (with the next stage's pieces and any prefetch) and
+    // published by a second barrier.
+    bool wreload = false;
+    if constexpr (WR) {
+      if (ct.n0 != wblk) {
+        load_w(ct.n0);
+        wreload = true;
+      }
+    }
     if (pdi >= 0) {
       if (ppre) settle();
       flush(ptl, pdi, pall, ppre, lds + ((decltype(slot_c)::value + 2) % 3) * RSLOT);
+    }
+    if (WR && wreload) {
+      roll_wait_vmcnt<0>();
+      asm volatile("s_barrier" ::: "memory");
     }
     const int di = ct.di_lo + cs;
     // the output depth this slice completes: 2-D di + pd, 3-D the bank of di + pd - 2
@@ -808,7 +889,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       tk0 = a.sptap[ct.n0 >> 5];
       tk1 = a.sptap[(ct.n0 >> 5) + 1];
     }
-    compute(slot_c, di + a.pd, kd_mask(ct.z0, ct.z1, di), dn, vn, tnext, tc, tm, tk0, tk1);
+    compute(slot_c, di + a.pd, kd_mask(ct.z0, ct.z1, di), dn, vn, tnext, tc, tm, tk0, tk1, cc);
     if constexpr (PREF) {
       if (pf_next) {
         prefetch(ct, pz);
@@ -952,9 +1033,9 @@ int roll_num_cus() {
   return n;
 }
 
-template <int KD, int NT, int PRO, int EM, int SP, typename H>
+template <int KD, int NT, int PRO, int EM, int SP, typename H, int WR = 0>
 int launch_roll(const RollArgs& a, size_t lds, int grid, hipStream_t s) {
-  auto kern = conv_roll_kernel<KD, NT, PRO, EM, SP, H>;
+  auto kern = conv_roll_kernel<KD, NT, PRO, EM, SP, H, WR>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   kern<<<grid, RNW * 64, lds, s>>>(a);
   VSRK_LAUNCH_CHECK("conv_fwd(roll)");
@@ -1123,9 +1204,25 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   const int64_t ntiles = spatial * nzc;
   VSRK_CHECK(ntiles < (1ll << 31), "conv_fwd(roll): too many tiles");
   a.ntiles = (int)ntiles;
-  const size_t slot = k3 ? RollGeo<3, 1>::SLOT : RollGeo<1, 2>::SLOT;
-  const size_t lds = (size_t)RNSLOT * slot + (size_t)a.cout_pad * 4 +
-                     (d->prologue || bnred ? 2 * (size_t)a.cin_pad * 4 : 0) + (bnred ? 4 * (size_t)a.cout_pad * 4 : 0);
+  // resident weights (WR): plain views, no prologue, the weight image of an
+  // output block <= 80 KB, and (2-D) one output block for the whole launch
+  // -- EDSR's 64 -> 64 body convs -- or (3-D) whole-depth tiles, where a
+  // reload per tile is amortised over nsl x nchunk stages (DUF's data
+  // gradients 32 -> F).  VSRK_ROLL_WRES=0 turns it off (A/B).
+  static int wres_mode = -1;
+  if (wres_mode < 0) {
+    const char* e = getenv("VSRK_ROLL_WRES");
+    wres_mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  const size_t nb = k3 ? RollGeo<3, 1>::NB : RollGeo<1, 2>::NB;
+  const size_t wbytes = (size_t)a.nchunk * nb * 1024;
+  const size_t tables = (size_t)a.cout_pad * 4 + (d->prologue || bnred ? 2 * (size_t)a.cin_pad * 4 : 0) +
+                        (bnred ? 4 * (size_t)a.cout_pad * 4 : 0);
+  const size_t wslot = k3 ? RollGeo<3, 1, 1>::SLOT : RollGeo<1, 2, 1>::SLOT;
+  const bool wr = wres_mode && sp == SP_NONE && !d->prologue && wbytes <= 80 * 1024 &&
+                  (k3 ? dzc == y->d : ntn == 1) && (size_t)RNSLOT * wslot + wbytes + tables <= 160 * 1024;
+  const size_t slot = wr ? wslot : (k3 ? RollGeo<3, 1>::SLOT : RollGeo<1, 2>::SLOT);
+  const size_t lds = (size_t)RNSLOT * slot + (wr ? wbytes : 0) + tables;
   if (bnred) {
     if (bnred->ws_floats < (size_t)ntiles * RNW * 64) return 0;
     a.bnx = (const char*)bnred->bnx->ptr;
@@ -1149,8 +1246,13 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   int rc = vsrk_dispatch16(x->dtype, [&](auto tag) {
     using H = decltype(tag);
     if (k3) {
-      if (bnred) return launch_roll<3, 1, 0, RE_BNRED, SP_NONE, H>(a, lds, grid, s);
+      if (bnred)
+        return wr ? launch_roll<3, 1, 0, RE_BNRED, SP_NONE, H, 1>(a, lds, grid, s)
+                  : launch_roll<3, 1, 0, RE_BNRED, SP_NONE, H>(a, lds, grid, s);
       if (d->prologue) return relu ? launch_roll<3, 1, 1, RE_RELU, SP_NONE, H>(a, lds, grid, s) : launch_roll<3, 1, 1, 0, SP_NONE, H>(a, lds, grid, s);
+      if (wr)
+        return relu ? launch_roll<3, 1, 0, RE_RELU, SP_NONE, H, 1>(a, lds, grid, s)
+                    : launch_roll<3, 1, 0, 0, SP_NONE, H, 1>(a, lds, grid, s);
       return relu ? launch_roll<3, 1, 0, RE_RELU, SP_NONE, H>(a, lds, grid, s) : launch_roll<3, 1, 0, 0, SP_NONE, H>(a, lds, grid, s);
     }
     // 2-D forms of the EDSR body and its backward: plain, ReLU, residual,
@@ -1176,6 +1278,17 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
         case RE_PRELU: return launch_roll<1, 2, 0, RE_PRELU, SP_Y, H>(a, lds, grid, s);
         case RE_ACC: return launch_roll<1, 2, 0, RE_ACC, SP_Y, H>(a, lds, grid, s);
         case RE_PMASK: return launch_roll<1, 2, 0, RE_PMASK, SP_Y, H>(a, lds, grid, s);
+        default: return (int)VSRK_ERR_UNSUPPORTED;
+      }
+    }
+    if (wr) {
+      switch (em) {
+        case 0: return launch_roll<1, 2, 0, 0, SP_NONE, H, 1>(a, lds, grid, s);
+        case RE_RELU: return launch_roll<1, 2, 0, RE_RELU, SP_NONE, H, 1>(a, lds, grid, s);
+        case RE_RES: return launch_roll<1, 2, 0, RE_RES, SP_NONE, H, 1>(a, lds, grid, s);
+        case RE_MASK: return launch_roll<1, 2, 0, RE_MASK, SP_NONE, H, 1>(a, lds, grid, s);
+        case RE_RES | RE_ACC: return launch_roll<1, 2, 0, RE_RES | RE_ACC, SP_NONE, H, 1>(a, lds, grid, s);
+        case RE_PMASK: return launch_roll<1, 2, 0, RE_PMASK, SP_NONE, H, 1>(a, lds, grid, s);
         default: return (int)VSRK_ERR_UNSUPPORTED;
       }
     }
