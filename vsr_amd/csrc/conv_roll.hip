@@ -81,18 +81,6 @@ constexpr int RNSLOT = 3;
 #define ROLL_PFASM 0
 #endif
 
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void glds16_m0(const void* gsrc, uint32_t lds_base) {
-  asm volatile(
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %0, off"
-      :
-      : "v"(gsrc), "s"(lds_base)
-      : "memory", "m0");
-}
-#pragma clang diagnostic pop
 
 // Geometry of the two forms.  KD = 3, NT = 1: Conv3d 3x3x3, one 32-channel
 // output block, three accumulator banks (output depths).  KD = 1, NT = 2:
@@ -1219,7 +1207,11 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   const size_t tables = (size_t)a.cout_pad * 4 + (d->prologue || bnred ? 2 * (size_t)a.cin_pad * 4 : 0) +
                         (bnred ? 4 * (size_t)a.cout_pad * 4 : 0);
   const size_t wslot = k3 ? RollGeo<3, 1, 1>::SLOT : RollGeo<1, 2, 1>::SLOT;
-  const bool wr = wres_mode && sp == SP_NONE && !d->prologue && wbytes <= 80 * 1024 &&
+  // (2-D: not with a prefetched residual / mask operand -- those epilogues
+  // give wrong results with the two-pass park of the 24 KB WR slots, cause
+  // not found yet; tests/test_roll_gpu.py res / mask cases)
+  const bool pref2d = !k3 && ((residual != nullptr) != (mask != nullptr && !pmask)) && !d->accumulate;
+  const bool wr = wres_mode && sp == SP_NONE && !d->prologue && wbytes <= 80 * 1024 && !pref2d &&
                   (k3 ? dzc == y->d : ntn == 1) && (size_t)RNSLOT * wslot + wbytes + tables <= 160 * 1024;
   const size_t slot = wr ? wslot : (k3 ? RollGeo<3, 1>::SLOT : RollGeo<1, 2>::SLOT);
   const size_t lds = (size_t)RNSLOT * slot + (wr ? wbytes : 0) + tables;
@@ -1285,8 +1277,6 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
       switch (em) {
         case 0: return launch_roll<1, 2, 0, 0, SP_NONE, H, 1>(a, lds, grid, s);
         case RE_RELU: return launch_roll<1, 2, 0, RE_RELU, SP_NONE, H, 1>(a, lds, grid, s);
-        case RE_RES: return launch_roll<1, 2, 0, RE_RES, SP_NONE, H, 1>(a, lds, grid, s);
-        case RE_MASK: return launch_roll<1, 2, 0, RE_MASK, SP_NONE, H, 1>(a, lds, grid, s);
         case RE_RES | RE_ACC: return launch_roll<1, 2, 0, RE_RES | RE_ACC, SP_NONE, H, 1>(a, lds, grid, s);
         case RE_PMASK: return launch_roll<1, 2, 0, RE_PMASK, SP_NONE, H, 1>(a, lds, grid, s);
         default: return (int)VSRK_ERR_UNSUPPORTED;

@@ -228,6 +228,7 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
     return true;
   };
   const char* zp = reinterpret_cast<const char*>(g_wroll_zero);
+  asm volatile("" : "+v"(zp));  // the zero page address in a VGPR pair, not re-materialised per piece
   // DMA of walk w's stage into x slot xs / dy slot ys
   struct Dma {
     const H* xb;
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
     const H* base = ((qx >> q) & 1) ? d.xb : d.yb;
     const void* src = ((d.use >> q) & 1) ? (const void*)(base + rel[q]) : (const void*)zp;
     const int off = j < WNXP ? xs * WXSLOT + j * 1024 : j < WNP ? WDBASE + ys * WDSLOT + (j - WNXP) * 1024 : WJUNK;
-    glds16(src, (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds_addr(lds) + off)));
+    glds16_m0(src, (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds_addr(lds) + off)));
   };
   // BN-affine/ReLU prologue on this lane's own landed x piece q (in-image
   // pieces only: the halo stays zero, the conv pads relu(bn(x)))
