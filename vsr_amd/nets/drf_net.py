@@ -28,15 +28,17 @@ epilogue):
     gradient is accumulated from all its consumers into the matching slice of
     a gradient buffer of the concat layout, then one fused pass applies the
     PReLU derivative and reduces its slope gradient.
-  * Weight gradients over the whole sequence at once: the weights are shared
-    by all T frames (drf_net.py:38-49), so every conv's weight gradient is
-    one launch over the B*T samples after the recurrent backward, instead of
-    T per-frame launches of B samples and T split-reduces (VSR_DRF_SEQ_WGRAD=0
-    keeps the per-frame launches on the side stream).  For that, every
-    operand a weight gradient reads -- forward activations and backward
-    output gradients -- is frame t of a (B, T, h, w, C) sequence buffer, so
-    frames 0..T-1 form one strided view (depth = frame: a kd = 1 conv treats
-    depth as batch).
+  * Weight gradients over runs of frames: the weights are shared by all T
+    frames (drf_net.py:38-49), so a conv's weight gradient over K frames is
+    ONE launch over K*B samples.  Every operand a weight gradient reads --
+    forward activations and backward output gradients -- is frame t of a
+    frame-major (T, B, h, w, C) sequence buffer, so frames t..t+K-1 are K*B
+    consecutive samples of one view.  As the reverse-time backward finishes
+    frame t = 0 (mod K) the run's weight gradients are launched on the side
+    stream, overlapping the data-gradient chain of the frames still to go;
+    the runs accumulate in a fixed order (deterministic).  K keeps every
+    view's element offsets within 32 bits (7 at cfg 3), so the pipelined
+    kernels stay eligible.  VSR_DRF_SEQ_WGRAD=0: one launch per frame.
 """
 from __future__ import annotations
 
@@ -130,17 +132,17 @@ class _OutBlock(nn.Sequential):
 
 
 def _seq_view(views: list) -> torch.Tensor | None:
-    """Frames 0..T-1 of one sequence buffer as a single (B, T, h, w, C) view,
-    given the per-frame (B, 1, h, w, C) views in frame order; None when they
-    are not evenly spaced slices of one buffer."""
+    """Consecutive frames of one frame-major sequence buffer as a single
+    (K*B, 1, h, w, C) view, given the per-frame (B, 1, h, w, C) views in frame
+    order; None when they are not consecutive sample blocks of one buffer."""
     v0 = views[0]
-    sd = v0.stride(1)
+    b, _, h, w, c = v0.shape
+    sn = v0.stride(0)
     es = v0.element_size()
     for t, v in enumerate(views):
-        if v.shape != v0.shape or v.stride() != v0.stride() or v.data_ptr() != v0.data_ptr() + t * sd * es:
+        if v.shape != v0.shape or v.stride() != v0.stride() or v.data_ptr() != v0.data_ptr() + t * b * sn * es:
             return None
-    b, _, h, w, c = v0.shape
-    return torch.as_strided(v0, (b, len(views), h, w, c), v0.stride(), v0.storage_offset())
+    return torch.as_strided(v0, (len(views) * b, 1, h, w, c), v0.stride(), v0.storage_offset())
 
 
 class _DRFBase(BaseNet):
@@ -223,16 +225,16 @@ class _DRFBase(BaseNet):
                 return new(hh, ww, c)
             big = seqs.get(name)
             if big is None:
-                big = seqs[name] = torch.empty((b, nfr, hh, ww, c), dtype=cd, device=dev)
-            return big[:, t:t + 1]
+                big = seqs[name] = torch.empty((nfr, b, hh, ww, c), dtype=cd, device=dev)
+            return big[t].unsqueeze(1)
 
         XV = None
-        if seqs is not None:  # all input frames in one layout move
-            XV = F.to_view(torch.stack([x.float() for x in frames], dim=2), cd, cpad=8)[..., :cin]
+        if seqs is not None:  # all input frames in one layout move, frame-major
+            XV = F.to_view(torch.cat([x.float() for x in frames]), cd, cpad=8)[..., :cin]  # (T*b, 1, h, w, cin)
         outs, recs = [], []
         X0 = buf("X0", 0, h, w, 2 * f, T + 1)
         for t, x in enumerate(frames):
-            xv = XV[:, t:t + 1] if XV is not None else F.to_view(x, cd, cpad=8)[..., :cin]
+            xv = XV[t * b:(t + 1) * b] if XV is not None else F.to_view(x, cd, cpad=8)[..., :cin]
             u1 = buf("u1", t, h, w, 4 * f)
             F.conv(xv, pw(ib.conv1), u1, K3, P1, bias=ib.conv1.bias, act=PR, act_param=ib.prelu1.weight)
             F.conv(u1, pw(ib.conv2), X0[..., :f], K1, P0, bias=ib.conv2.bias, act=PR, act_param=ib.prelu2.weight)
@@ -323,11 +325,42 @@ class _DRFBase(BaseNet):
                 return new(hh, ww, c)
             big = seqs.get(name)
             if big is None:
-                big = seqs[name] = torch.empty((b, T, hh, ww, c), dtype=cd, device=dev)
-            return big[:, t:t + 1]
+                big = seqs[name] = torch.empty((T, b, hh, ww, c), dtype=cd, device=dev)
+            return big[t].unsqueeze(1)
 
-        # deferred weight gradients: key -> (launch(x, dy, accumulate), {frame: (x, dy)})
+        # deferred weight gradients: key -> (param, launch(x, dy, accumulate),
+        # {frame: (x, dy)}, runs launched, frames per run K)
         pend: dict = {}
+
+        def run_frames(x, dy) -> int:
+            """K for a weight: the run's view must keep 32-bit element offsets
+            (B x the frame's span of the wider operand, per frame)"""
+            span = max(v.stride(0) * b for v in (x, dy))
+            return max(1, min(T, (2 ** 31 - 1) // max(span, 1) - 1))
+
+        def launch_runs(t):
+            """frame t just finished: launch every deferred weight gradient
+            whose run [t, t + K) is complete on the side stream (accumulating
+            after its first run)"""
+            if not seq:
+                return
+            for key, (prm, launch, frs, nrun, K) in list(pend.items()):
+                if t % K != 0:
+                    continue
+                t1 = min(t + K, T)
+                xs = _seq_view([frs[u][0] for u in range(t, t1)])
+                dys = _seq_view([frs[u][1] for u in range(t, t1)])
+                if xs is not None and dys is not None:
+                    self._on_wgrad_stream(lambda: launch(xs, dys, nrun > 0), xs, dys)
+                    nrun += 1
+                else:  # operands not in sequence buffers: per frame
+                    for u in range(t, t1):
+                        x_, dy_ = frs[u]
+                        self._on_wgrad_stream(lambda: launch(x_, dy_, nrun > 0), x_, dy_)
+                        nrun += 1
+                for u in range(t, t1):
+                    del frs[u]
+                pend[key] = (prm, launch, frs, nrun, K)
 
         def gbuf(prm):
             key = id(prm)
@@ -344,7 +377,7 @@ class _DRFBase(BaseNet):
             if not seq:
                 self._on_wgrad_stream(lambda: launch(x, dy, acc), x, dy)
                 return
-            pend.setdefault(id(key), (key, launch, {}))[2][t] = (x, dy)
+            pend.setdefault(id(key), (key, launch, {}, 0, run_frames(x, dy)))[2][t] = (x, dy)
 
         def wgrad(conv, x, dy, ksz, pad, t, **kw):
             dw, acc = gbuf(conv.weight)
@@ -380,13 +413,13 @@ class _DRFBase(BaseNet):
         HH, WW = recs[0]["tail_in"].shape[2], recs[0]["tail_in"].shape[3]
         gfull = [gys[t] if t < len(gys) and gys[t] is not None else
                  torch.zeros((b, co, HH, WW), dtype=torch.float32, device=dev) for t in range(T)]
-        GV = F.to_view(torch.stack([g_.float() for g_ in gfull], dim=2), cd, cpad=8)[..., :co]  # (b, T, HH, WW, co)
+        GV = F.to_view(torch.cat([g_.float() for g_ in gfull]), cd, cpad=8)[..., :co]  # (T*b, 1, HH, WW, co)
         d_hidden = None  # grad of the previous frame's f_features (X0_t[..., f:])
         for t in range(T - 1, -1, -1):
             rc = recs[t]
             u = rc["tail_in"]
             hh, ww = u.shape[2], u.shape[3]
-            g = GV[:, t:t + 1]
+            g = GV[t * b:(t + 1) * b]
             tc = self._last_conv()
             wgrad(tc, u, g, K3, P1, t)
             ups = list(zip(self._ups(), rc["ups_in"]))
@@ -464,15 +497,7 @@ class _DRFBase(BaseNet):
             du1 = F.conv(gin, pw(ib.conv2, 1), sbuf("du_u1", t, h, w, 4 * f), K1, P0)
             prelu(rc["u1"], du1, ib.prelu1, du1)
             wgrad(ib.conv1, rc["xv"], du1, K3, P1, t)
-        # every shared weight's gradient once over the sequence (frames as depth)
-        for key, launch, frs in pend.values():
-            xs = _seq_view([frs[t][0] for t in range(T)])
-            dys = _seq_view([frs[t][1] for t in range(T)])
-            if xs is not None and dys is not None:
-                launch(xs, dys, False)
-            else:  # operands not in sequence buffers: per frame, accumulated
-                for t in range(T):
-                    launch(frs[t][0], frs[t][1], t > 0)
+            launch_runs(t)
         for prm, g in bufs.values():
             self._grad_done(grads, prm, g)
         return grads
