@@ -79,6 +79,10 @@ struct WRArgs {
 
 __device__ __attribute__((aligned(256))) uint4 g_wroll_zero[16];
 
+#ifndef WR_XWIN
+#define WR_XWIN 1
+#endif
+
 template <int N>
 __device__ __forceinline__ void wr_wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -292,8 +296,21 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
         f[kw] = tr_frag(xsl + ((xb[kw][0] + R * WHS * 64) ^ flip), xsl + ((xb[kw][1] + R * WHS * 64) ^ flip));
     };
     int qi = 0;
+    // x rows R = r + kh: each halo row feeds three (r, kh) pairs, so the
+    // three rows a dy row meets stay in registers (a sliding window of
+    // 3 rows x 3 kw fragments) and each row is read from LDS once per stage:
+    // 6 instead of 12 row reads (36 instead of 72 transposed reads per stage;
+    // the weight gradient is LDS-read bound).  WR_XWIN=0: the old form.
+#if WR_XWIN
+    uint4 xw[3][3];
+    load_x(xw[0], 0);
+    load_x(xw[1], 1);
+#endif
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+#if WR_XWIN
+      load_x(xw[(r + 2) % 3], r + 2);
+#endif
       uint4 yf[3];
 #pragma unroll
       for (int kd = 0; kd < 3; ++kd) {
@@ -305,17 +322,26 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
         if (qi < WNQ && don) dma(dn, qi, xs2, ys2);
       }
       if constexpr (PRO) {
-        if (r == 3 && tnext) {
-          if (don) wr_wait_vmcnt<WNQ>();
-          else wr_wait_vmcnt<0>();
+        // the next stage's x pieces: waited for once this stage's pieces are
+        // all issued (row 2), transformed two per row over rows 2 and 3
+        // (one burst in row 3 cost ~30 % of the kernel beside the prologue-free form)
+        if (r >= 2 && tnext) {
+          if (r == 2) {
+            if (don) wr_wait_vmcnt<WNQ>();
+            else wr_wait_vmcnt<0>();
+          }
 #pragma unroll
-          for (int q = 0; q < 4; ++q) transform_piece((XS + 1) % 3, q, tm);
+          for (int q = 2 * (r - 2); q < 2 * (r - 1); ++q) transform_piece((XS + 1) % 3, q, tm);
         }
       }
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
+#if WR_XWIN
+        const uint4* xf = xw[(r + kh) % 3];
+#else
         uint4 xf[3];
         load_x(xf, r + kh);
+#endif
 #pragma unroll
         for (int kd = 0; kd < 3; ++kd) {
           if ((km >> kd) & 1) {
