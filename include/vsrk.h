@@ -160,8 +160,11 @@ int vsrk_conv_set_algo(int32_t mode);
  * forward, data gradient and weight gradient in one pass over HBM, default
  * on), "thin" (cin <= 4 / cout <= 3 kernels incl. their weight gradient,
  * default on), "wgrad_pipe" (pipelined 16-bit 3x3(x3) weight gradient, default
- * on); mode -1 = default/environment (VSRK_CONV_FAST, VSRK_CONV_PW,
- * VSRK_CONV_ROLL, VSRK_CONV_THIN, VSRK_WGRAD_PIPE), 0 = off, 1 = on where eligible.  Every path computes the
+ * on), "wgrad_roll" (rolling-depth Conv3d 3x3x3 weight gradient), "wgrad_row"
+ * (rolling-row Conv2d 3x3 weight gradient over 64 x 64 channel blocks,
+ * default on); mode -1 = default/environment (VSRK_CONV_FAST, VSRK_CONV_PW,
+ * VSRK_CONV_ROLL, VSRK_CONV_THIN, VSRK_WGRAD_PIPE, VSRK_WGRAD_ROLL,
+ * VSRK_WGRAD_ROW), 0 = off, 1 = on where eligible.  Every path computes the
  * same result as the generic kernels within bf16 rounding. */
 int vsrk_conv_set_path(const char* path, int32_t mode);
 
@@ -369,6 +372,23 @@ typedef struct vsrk_bn_contrib {
 } vsrk_bn_contrib;
 int vsrk_bn_relu_bwd_apply_multi(const vsrk_tensor5* x, const vsrk_tensor5* dx, int32_t accumulate, int32_t n,
                                  const vsrk_bn_contrib* contribs, void* stream);
+
+/* vsrk_conv_fwd_reduce mode 2 (a square 1x1x1 data gradient with the next
+ * BatchNorm+ReLU backward's sums in its store pass) whose input is itself a
+ * BN+ReLU backward apply, computed in the operand load: DUF's dense unit,
+ * bn2's apply feeding conv1's data gradient (duf_net.py:198-201).
+ *   x_out = vsrk_bn_relu_bwd_apply(bn_x, pre->dz, pre's BN)   (bitwise)
+ *   y     = conv(x_out), (out_a, out_b) = bnx's BN+ReLU backward sums of y
+ * pre->scale is not read: the mask uses gamma * invstd, which is
+ * vsrk_bn_finalize's scale; pre->d0 is ignored.  bn_x, pre->dz and x_out
+ * share one geometry (N, D, H, W, C with C % 32 == 0, 64..224); y may alias
+ * pre->dz (each tile's rows are read before they are written).
+ * VSRK_ERR_UNSUPPORTED when not eligible (nothing launched). */
+int vsrk_conv_fwd_reduce_bnb(const vsrk_conv_desc* desc, const vsrk_tensor5* bn_x, const vsrk_bn_contrib* pre,
+                             const vsrk_tensor5* x_out, const void* w_packed, const vsrk_tensor5* y,
+                             const vsrk_tensor5* bnx, const float* scale, const float* shift, const float* mean,
+                             const float* invstd, float* out_a, float* out_b, void* workspace,
+                             size_t workspace_bytes, void* stream);
 
 /* DUF dynamic upsampling (duf_net.py:67-97), fused: softmax over the k*k taps
  * of per-pixel logits (n, h, w, k*k*r*r) fp32 (tap-major, as the reference's

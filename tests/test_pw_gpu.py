@@ -318,3 +318,54 @@ def test_pw_fused_reduce_unsupported_shape_launches_nothing():
     wp = F.pack_weight(torch.randn((256, 256, 1, 1, 1), device=DEV), 1, BF)
     assert F.conv_reduce(x, wp, y, bnx=x, st=torch.ones((4, 256), device=DEV)) is None
     assert (y == 3.0).all()
+
+
+@pytest.mark.parametrize("c", [64, 96, 128, 160, 192, 224])
+@pytest.mark.parametrize("alias,hw", [(False, (9, 37)), (True, (9, 37)), (True, (8, 32))])
+def test_pw_fused_reduce_bnb(c, alias, hw, grid_cap):
+    """vsrk_conv_fwd_reduce_bnb: DUF's conv1 data gradient whose input is
+    bn2's BN+ReLU backward apply, computed in the operand load
+    (duf_net.py:198-201), with bn1's backward reduce in the store pass.  The
+    applied gradient (x_out, the weight gradient's dY) equals
+    bn_relu_bwd_apply bitwise, the conv output equals apply + conv bitwise
+    (also written over the input gradient's own storage, as the net does),
+    the sums match the separate reduction within fp32 summation noise, and
+    a second launch repeats them bitwise."""
+    g = torch.Generator().manual_seed(c + 7 * alias + hw[1])
+    (n, D), (h, w) = (2, 5), hw  # 8 x 32: whole tiles per sample (the aligned kernel form)
+    big = torch.randn((n, D, h, w, c + 32), generator=g).to(DEV, BF)
+    R = big[:, 1:4, :, :, :c]                     # bn1's input (a concat-buffer view)
+    t1 = torch.randn((n, 3, h, w, c + 16), generator=g).to(DEV, BF)[..., 8:8 + c]  # bn2's input, strided
+    dz2 = torch.randn((n, 3, h, w, c), generator=g).to(DEV, BF)
+    wt = (torch.randn((c, c, 1, 1, 1), generator=g) / c ** 0.5).to(DEV)
+    wp = F.pack_weight(wt, 1, BF)
+
+    def bn_consts():
+        gm = (torch.rand(c, generator=g) + 0.5).to(DEV)
+        ist = (torch.rand(c, generator=g) + 0.5).to(DEV)
+        mu = (torch.randn(c, generator=g) * 0.1).to(DEV)
+        sh = torch.randn(c, generator=g).to(DEV) * 0.5
+        return gm, torch.stack([gm * ist, sh, mu, ist])  # scale = gamma * invstd, as bn_finalize
+
+    gm2, st2 = bn_consts()
+    _, st1 = bn_consts()
+    red2 = torch.randn((2, c), generator=g).to(DEV) * 50
+    count = 1234.0
+    dt1_ref = torch.empty_like(dz2)
+    F.bn_relu_bwd_apply(t1, dz2, st2, gm2, red2, count, dt1_ref, False)
+    y_ref = torch.empty_like(dz2)
+    F.conv(dt1_ref, wp, y_ref, (1, 1, 1), (0, 0, 0))
+    ref = F.bn_relu_bwd_reduce(R, y_ref, st1)
+    outs = []
+    for _ in range(2):
+        dz = dz2.clone()
+        dt1 = torch.empty_like(dz2)
+        y = dz if alias else torch.empty_like(dz2)
+        red = F.conv_reduce_bnb(t1, dz, st2, gm2, red2, count, dt1, wp, y, bnx=R, st=st1)
+        assert red is not None
+        assert torch.equal(dt1, dt1_ref)
+        assert torch.equal(y, y_ref)
+        outs.append(red)
+    err = (outs[0] - ref).abs().max().item()
+    assert err <= 1e-5 * (1 + ref.abs().max().item()), err
+    assert torch.equal(outs[0], outs[1])

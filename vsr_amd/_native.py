@@ -80,6 +80,8 @@ _SIGS = {
     "vsrk_conv_fwd_prelu_bwd": (C.c_int, [_CD, _T5, _P, _P, _T5, _T5, _P, C.c_int32, _P, C.c_size_t, _P]),
     "vsrk_conv_fwd_reduce": (C.c_int, [_CD, _T5, _P, _P, _P, _P, _T5, C.c_int32, _T5, _P, _P, _P, _P, _P, _P, _P,
                                        C.c_size_t, _P]),
+    "vsrk_conv_fwd_reduce_bnb": (C.c_int, [_CD, _T5, C.POINTER(BnContrib), _T5, _P, _T5, _T5, _P, _P, _P, _P, _P,
+                                           _P, _P, C.c_size_t, _P]),
     "vsrk_conv_wgrad_workspace_size": (C.c_size_t, [_CD, _T5, _T5]),
     "vsrk_conv_wgrad": (C.c_int, [_CD, _T5, _T5, _P, _P, C.c_float, C.c_int32, _P, _P, C.c_int32, _P,
                                   C.c_size_t, _P]),

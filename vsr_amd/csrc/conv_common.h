@@ -306,6 +306,19 @@ int vsrk_conv_wgrad_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const v
                          int* nsplit_out, hipStream_t s);
 void vsrk_conv_set_wgrad_roll_mode(int mode);
 extern int vsrk_g_roll_dz;  // vsrk_conv_set_roll_depth (conv_roll.hip)
+// rolling-row 16-bit Conv2d 3x3 weight gradient (conv_wgrad_row.hip): plan
+// (false = not eligible) and launch (1 = launched the slab kernel, whose slabs
+// wgrad_reduce_kernel sums over nsplit splits and ncot * ncic combos of
+// cot_w x 64 channels; 0 = not eligible)
+struct VsrkRowPlan {
+  int bands, band_h, nseg, ncot, ncic, nsplit;
+  int cot_w, slab;  // output channels per combo, floats per slab
+  size_t ws_bytes;
+};
+bool vsrk_wgrad_row_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk_tensor5* dy, VsrkRowPlan* p);
+int vsrk_conv_wgrad_row(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk_tensor5* dy, int want_bias,
+                        float* ws, size_t ws_bytes, VsrkRowPlan* plan, hipStream_t s);
+void vsrk_conv_set_wgrad_row_mode(int mode);
 // thin-channel weight gradient (conv_thin.hip): 1 = launched the slab kernel, 0 = not eligible.
 int vsrk_conv_wgrad_thin(const vsrk_conv::WgradArgs& a, int nco, int nci, int perm_r, int dtype, hipStream_t s);
 

@@ -46,7 +46,9 @@ extern "C" int vsrk_conv_set_path(const char* path, int32_t mode) {
   else if (p == "pw") vsrk_g_pw_mode = mode;
   else if (p == "roll") vsrk_conv_set_roll_mode(mode);
   else if (p == "wgrad_roll") vsrk_conv_set_wgrad_roll_mode(mode);
-  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, pw, roll, thin, wgrad_pipe, wgrad_roll)", path);
+  else if (p == "wgrad_row") vsrk_conv_set_wgrad_row_mode(mode);
+  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, pw, roll, thin, wgrad_pipe, wgrad_roll, wgrad_row)",
+                  path);
   return VSRK_OK;
 }
 

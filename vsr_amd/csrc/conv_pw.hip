@@ -35,6 +35,9 @@ using namespace vsrk_conv;
 
 constexpr int PW_THR = 256;  // 4 waves, one per SIMD
 constexpr int PW_KP = 64;    // wgrad voxels per stage
+#ifndef PW_BXPRE
+#define PW_BXPRE 1  // fused BN-backward reduce: BN input rows loaded ahead of the MFMAs (0: in the store pass)
+#endif
 
 static bool pw_enabled() {
   if (vsrk_g_pw_mode < 0) {
@@ -139,6 +142,14 @@ struct PwArgs {  // 16-bit tensors of one type H (bf16 / fp16)
   int64_t bsn, bsw;
   const float *bsc, *bsh, *bmu, *bis;
   float* red_ws;
+  // BNB: the conv input is a BatchNorm+ReLU backward applied on the fly
+  // (x = dz, the BN's output gradient; qx = the BN's input): the applied
+  // gradient feeds the MFMAs and is stored to xo (the weight gradient's dY)
+  const void* qx;
+  void* xo;
+  int64_t qsn, qsw, osn, osw;
+  const float *qsh, *qmu, *qis, *qgm, *qsdy, *qsdyx;
+  float qinv_count;
   int64_t xsn, xsw, ysn, ysw, msn, msw;  // element strides
   int nvox, dhw;
   FastDiv fd;                             // division by dhw
@@ -350,7 +361,13 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
 // kernel read them 8 bytes per lane across 32 voxel rows).  The buffered
 // value is rounded to H before the accumulate: one extra rounding of the new
 // term against the tile kernel.
-template <int NCB, int NKB, int M, bool PRO, bool AL, int ACT, bool EIN, typename H, int RED = 0>
+// BNB (with RED 2, no PRO / bias): the input is the BN+ReLU backward of the
+// previous BatchNorm, x' = k1 * (qx * k1 + sh > 0 ? x : 0) + k2 * qx + k3
+// per channel (bn_relu_bwd_apply_kernel's arithmetic, so x' is bitwise the
+// separate apply's; k1 = gamma * invstd is bn_finalize's scale, bn.hip:193),
+// computed on the 16-byte row chunks between the coalesced loads and the LDS
+// put, and stored once to xo for the weight gradient.
+template <int NCB, int NKB, int M, bool PRO, bool AL, int ACT, bool EIN, typename H, int RED = 0, bool BNB = false>
 __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
   const H* aX = reinterpret_cast<const H*>(a.x);
   H* aY = reinterpret_cast<H*>(a.y);
@@ -367,11 +384,16 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
   char* lw = lds;                                         // [KS][2][COP] x 16 B
   float* lsc = reinterpret_cast<float*>(lds + WBYTES);    // [CIP]
   float* lsh = lsc + CIP;                                 // [CIP]
-  float* lb = reinterpret_cast<float*>(lds + WBYTES + (PRO ? 2 * CIP * 4 : 0));  // [COP]
+  static_assert(!BNB || (RED == 2 && !PRO && !EIN && ACT == 0), "BNB: the data-gradient reduce form only");
+  constexpr int OFF_LB = WBYTES + (PRO ? 2 * CIP * 4 : 0);
+  constexpr int OFF_Q = OFF_LB + (BNB ? 0 : COP * 4);    // BNB: no bias (a data gradient)
+  constexpr int OFF_BUF = OFF_Q + (BNB ? 4 * CIP * 4 : 0);
+  float* lb = reinterpret_cast<float*>(lds + OFF_LB);     // [COP]
+  float* lq = reinterpret_cast<float*>(lds + OFF_Q);      // BNB: [4][CIP] sh, k1, k2, k3
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int hf = lane >> 5, col = lane & 31;
   const int co0 = blockIdx.y * COP;
-  char* buf = lds + WBYTES + (PRO ? 2 * CIP * 4 : 0) + COP * 4 + wave * (ROWS * RS);
+  char* buf = lds + OFF_BUF + wave * (ROWS * RS);
 
   for (int i = tid; i < KS * 2 * COP; i += PW_THR) {
     const int co = i % COP, t = i / COP, h = t & 1, s = t >> 1;
@@ -382,7 +404,25 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
     *reinterpret_cast<uint4*>(lw + i * 16) = v;
   }
   if (PRO) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, CIP, tid, PW_THR);
-  for (int i = tid; i < COP; i += PW_THR) lb[i] = (a.bias && co0 + i < a.cout) ? a.bias[co0 + i] : 0.f;
+  if constexpr (BNB) {
+    for (int c = tid; c < CIP; c += PW_THR) {
+      float sh = 0.f, k1 = 0.f, k2 = 0.f, k3 = 0.f;
+      if (c < a.cin) {  // bn_relu_bwd_apply_kernel's constants, the same fp32 operations
+        const float is = a.qis[c], gm = a.qgm ? a.qgm[c] : 1.f;
+        const float aa = gm * is, bb = is * a.qsdyx[c] * a.qinv_count;
+        sh = a.qsh[c];
+        k1 = aa;
+        k2 = -aa * bb;
+        k3 = aa * (a.qmu[c] * bb - a.qsdy[c] * a.qinv_count);
+      }
+      lq[c] = sh;
+      lq[CIP + c] = k1;
+      lq[2 * CIP + c] = k2;
+      lq[3 * CIP + c] = k3;
+    }
+  } else {
+    for (int i = tid; i < COP; i += PW_THR) lb[i] = (a.bias && co0 + i < a.cout) ? a.bias[co0 + i] : 0.f;
+  }
   __syncthreads();
 
   const bool relu_in = (a.prologue & VSRK_PRO_RELU) != 0;
@@ -422,7 +462,8 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
   // fixed chunk roles: chunk k of a lane = row (lane + 64k) / CPR, column % CPR.
   // `ln` = lane through an opaque copy per use site: the per-chunk offsets
   // derived from it are recomputed (a few VALU) instead of held in VGPRs.
-  auto load = [&](int tile, uint4 (&r)[NCK]) __attribute__((always_inline)) {
+  constexpr int NQK = BNB ? NCK : 1;
+  auto load = [&](int tile, uint4 (&r)[NCK], uint4 (&rq)[NQK]) __attribute__((always_inline)) {
     int ln = lane;
     asm volatile("" : "+v"(ln));
     const int v0 = tile * ROWS;
@@ -434,24 +475,82 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
       const uint32_t off = row_off(tb, row, v0, a.xsn, a.xsw);
       r[k] = bload16(rs, c < a.cin ? off + 2 * c : PW_OOB);
     }
+    if constexpr (BNB) {
+      const Rsrc rq_ = rsrc_at(reinterpret_cast<const H*>(a.qx) + (int64_t)tb.n0 * a.qsn);
+#pragma unroll
+      for (int k = 0; k < NCK; ++k) {
+        const int i = ln + 64 * k, row = i / CPR, c = 8 * (i % CPR);
+        const uint32_t off = row_off(tb, row, v0, a.qsn, a.qsw);
+        rq[k] = bload16(rq_, c < a.cin ? off + 2 * c : PW_OOB);
+      }
+    }
   };
-  auto put = [&](const uint4 (&r)[NCK]) __attribute__((always_inline)) {
+  auto put = [&](int tile, const uint4 (&r)[NCK], const uint4 (&rq)[NQK]) __attribute__((always_inline)) {
     int ln = lane;
     asm volatile("" : "+v"(ln));
+    if constexpr (BNB) {
+      const int v0 = tile * ROWS;
+      const TileBase tb = tile_base(v0, a.fd);
+      const Rsrc ro = rsrc_at(reinterpret_cast<H*>(a.xo) + (int64_t)tb.n0 * a.osn);
+      const uint32_t qb = lds_addr(lq);
 #pragma unroll
-    for (int k = 0; k < NCK; ++k) {
-      const int i = ln + 64 * k, row = i / CPR, c = i % CPR;
-      *reinterpret_cast<uint4*>(buf + row * RS + c * 16) = r[k];
+      for (int k = 0; k < NCK; ++k) {
+        const int i = ln + 64 * k, row = i / CPR, c = i % CPR;
+        float g[8], f[8], o[8], sh[8], k1[8], k2[8], k3[8];
+        Chunk<H>::unpack(r[k], g);
+        Chunk<H>::unpack(rq[k], f);
+        const uint32_t qa = qb + c * 32;
+        *reinterpret_cast<float4*>(sh) = lds_ldf4(qa);
+        *reinterpret_cast<float4*>(sh + 4) = lds_ldf4(qa + 16);
+        *reinterpret_cast<float4*>(k1) = lds_ldf4(qa + CIP * 4);
+        *reinterpret_cast<float4*>(k1 + 4) = lds_ldf4(qa + CIP * 4 + 16);
+        *reinterpret_cast<float4*>(k2) = lds_ldf4(qa + CIP * 8);
+        *reinterpret_cast<float4*>(k2 + 4) = lds_ldf4(qa + CIP * 8 + 16);
+        *reinterpret_cast<float4*>(k3) = lds_ldf4(qa + CIP * 12);
+        *reinterpret_cast<float4*>(k3 + 4) = lds_ldf4(qa + CIP * 12 + 16);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dy = fmaf(f[e], k1[e], sh[e]) > 0.f ? g[e] : 0.f;
+          o[e] = fmaf(k1[e], dy, fmaf(k2[e], f[e], k3[e]));
+        }
+        const uint4 v = Chunk<H>::pack(o);
+        *reinterpret_cast<uint4*>(buf + row * RS + c * 16) = v;
+        const uint32_t off = row_off(tb, row, v0, a.osn, a.osw);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), ro,
+                                               (int)(8 * c < a.cin ? off + 16 * c : PW_OOB), 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NCK; ++k) {
+        const int i = ln + 64 * k, row = i / CPR, c = i % CPR;
+        *reinterpret_cast<uint4*>(buf + row * RS + c * 16) = r[k];
+      }
     }
   };
 
-  uint4 rg[NCK];
+  uint4 rg[NCK], rgq[NQK];
   int t = blockIdx.x * (PW_THR / 64) + wv;
-  if (t < a.ntiles) load(t, rg);
+  if (t < a.ntiles) load(t, rg, rgq);
   while (t < a.ntiles) {
     const int tn = t + nwaves;
-    put(rg);
-    if (tn < a.ntiles) load(tn, rg);  // in flight during this tile's MFMAs and stores
+    put(t, rg, rgq);
+    // RED 2: the BN input rows of this tile's reduce, issued before the next
+    // tile's operands so the epilogue's wait on them leaves those in flight
+    uint4 bx[RED == 2 ? RNIT : 1];
+    const bool lane_ok = lane < ROCPR * RSTEP;
+    auto load_bx = [&]() __attribute__((always_inline)) {
+      const int v0 = t * ROWS;
+      const TileBase tb = tile_base(v0, a.fd);
+      const Rsrc rb = rsrc_at(reinterpret_cast<const H*>(a.bnx) + (int64_t)tb.n0 * a.bsn);
+#pragma unroll
+      for (int j = 0; j < RNIT; ++j) {
+        const int row = rrow0 + RSTEP * j;
+        const bool ok = lane_ok && row < ROWS && rch_ok;
+        bx[j] = bload16(rb, ok ? row_off(tb, row, v0, a.bsn, a.bsw) + 2 * (co0 + 8 * rcol) : PW_OOB);
+      }
+    };
+    if constexpr (RED == 2 && PW_BXPRE) load_bx();
+    if (tn < a.ntiles) load(tn, rg, rgq);  // in flight during this tile's MFMAs and stores
 
     f32x16 acc[M][NCB];
 #pragma unroll
@@ -510,7 +609,8 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
       for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float4 bb = lds_ldf4(bias_b + (cb * 32 + 8 * j) * 4);
+          float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
+          if constexpr (!BNB) bb = lds_ldf4(bias_b + (cb * 32 + 8 * j) * 4);
 #pragma unroll
           for (int m = 0; m < M; ++m) {
             float o[4] = {acc[m][cb][4 * j] + bb.x, acc[m][cb][4 * j + 1] + bb.y, acc[m][cb][4 * j + 2] + bb.z,
@@ -532,17 +632,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
       const int v0 = t * ROWS;
       const TileBase tb = tile_base(v0, a.fd);
       const Rsrc ry = rsrc_at(aY + (int64_t)tb.n0 * a.ysn);
-      const Rsrc rb = rsrc_at(reinterpret_cast<const H*>(RED == 2 ? a.bnx : a.y) + (int64_t)tb.n0 * a.bsn);
-      const bool lane_ok = lane < ROCPR * RSTEP;
-      uint4 bx[RNIT];
-      if constexpr (RED == 2) {
-#pragma unroll
-        for (int j = 0; j < RNIT; ++j) {
-          const int row = rrow0 + RSTEP * j;
-          const bool ok = lane_ok && row < ROWS && rch_ok;
-          bx[j] = bload16(rb, ok ? row_off(tb, row, v0, a.bsn, a.bsw) + 2 * (co0 + 8 * rcol) : PW_OOB);
-        }
-      }
+      if constexpr (RED == 2 && !PW_BXPRE) load_bx();
 #pragma unroll
       for (int j = 0; j < RNIT; ++j) {
         const int row = rrow0 + RSTEP * j;
@@ -688,13 +778,14 @@ __global__ __launch_bounds__(256) void pw_red_final_kernel(const float* __restri
 // one output chunk): RED 1 with the BN prologue (a BatchNorm's input
 // statistics, duf_net.py:198-201), RED 2 without (the data gradient that
 // feeds a BN+ReLU backward, duf_net.py:198-200).
-template <int NCB, int M, int RED, typename H>
+template <int NCB, int M, int RED, typename H, bool BNB = false>
 static bool launch_fwd_reduce(const PwArgs& a, int grid, hipStream_t s) {
   constexpr int KS = 2 * NCB, COP = 32 * NCB, CIP = 16 * KS;
-  const size_t lds = (size_t)KS * 2 * COP * 16 + (RED == 1 ? 2 * CIP * 4 : 0) + COP * 4 + 4 * (32 * M) * (2 * CIP + 16);
+  const size_t lds = (size_t)KS * 2 * COP * 16 + (RED == 1 ? 2 * CIP * 4 : 0) + (BNB ? 4 * CIP * 4 : COP * 4) +
+                     4 * (32 * M) * (2 * CIP + 16);
   const bool al = a.dhw % (32 * M) == 0;
-  auto kern = al ? pw_fwd_staged_kernel<NCB, NCB, M, RED == 1, true, 0, false, H, RED>
-                 : pw_fwd_staged_kernel<NCB, NCB, M, RED == 1, false, 0, false, H, RED>;
+  auto kern = al ? pw_fwd_staged_kernel<NCB, NCB, M, RED == 1, true, 0, false, H, RED, BNB>
+                 : pw_fwd_staged_kernel<NCB, NCB, M, RED == 1, false, 0, false, H, RED, BNB>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   kern<<<dim3(grid, 1), PW_THR, lds, s>>>(a);
   return true;
@@ -1173,15 +1264,16 @@ extern "C" size_t vsrk_conv_fwd_reduce_workspace(const vsrk_conv_desc* d, const 
   return pw;
 }
 
-extern "C" int vsrk_conv_fwd_reduce(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed,
-                                    const float* bias, const float* pro_scale, const float* pro_shift,
-                                    const vsrk_tensor5* y, int32_t mode, const vsrk_tensor5* bnx, const float* scale,
-                                    const float* shift, const float* mean, const float* invstd, float* out_a,
-                                    float* out_b, void* workspace, size_t workspace_bytes, void* stream) {
+// q (with qx, xo): the BNB input form (vsrk_conv_fwd_reduce_bnb), x = q->dz
+static int fwd_reduce_impl(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                           const float* pro_scale, const float* pro_shift, const vsrk_tensor5* y, int32_t mode,
+                           const vsrk_tensor5* bnx, const float* scale, const float* shift, const float* mean,
+                           const float* invstd, float* out_a, float* out_b, void* workspace, size_t workspace_bytes,
+                           void* stream, const vsrk_tensor5* qx, const vsrk_bn_contrib* q, const vsrk_tensor5* xo) {
   VSRK_CHECK(d && x && y && w_packed && out_a && out_b, "conv_fwd_reduce: null argument");
   VSRK_CHECK(mode == 1 || mode == 2, "conv_fwd_reduce: mode must be 1 (statistics) or 2 (BN+ReLU backward)");
   hipStream_t s = (hipStream_t)stream;
-  if (mode == 2 && d->kd == 3) {
+  if (mode == 2 && d->kd == 3 && !q) {
     // the data gradient of a dense unit's Conv3d 3x3x3 (conv2) feeding bn2's
     // backward: the rolling kernel's epilogue form (conv_roll.hip)
     VSRK_CHECK(bnx && scale && shift && mean && invstd, "conv_fwd_reduce: mode 2 needs bnx and the BN constants");
@@ -1213,8 +1305,35 @@ extern "C" int vsrk_conv_fwd_reduce(const vsrk_conv_desc* d, const vsrk_tensor5*
         bnx->c != y->c || !dhw_dense(bnx) || !chunk_ok(bnx, 2))
       return VSRK_ERR_UNSUPPORTED;
   }
+  auto same_geo = [&](const vsrk_tensor5* t) {
+    return t->dtype == x->dtype && t->n == x->n && t->d == x->d && t->h == x->h && t->w == x->w && t->c == x->c &&
+           dhw_dense(t) && chunk_ok(t, 2);
+  };
+  if (q) {
+    if (mode != 2 || bias || d->prologue != VSRK_PRO_NONE || !same_geo(qx) || !same_geo(xo)) return VSRK_ERR_UNSUPPORTED;
+    VSRK_CHECK(q->shift && q->mean && q->invstd && q->sum_dy && q->sum_dy_xhat && q->count > 0,
+               "conv_fwd_reduce_bnb: missing BatchNorm operands");
+  }
   PwArgs a;
   if (!pw_fill_args(a, d, x, w_packed, bias, pro_scale, pro_shift, nullptr, y, x->c)) return VSRK_ERR_UNSUPPORTED;
+  if (q) {
+    const int64_t span_n = 32 * 4 / std::max(a.dhw, 1) + 2;
+    for (const vsrk_tensor5* t : {qx, xo})
+      if (2 * (span_n * t->sn + (int64_t)a.dhw * t->sw + t->c) >= 0x7FFFFFF0ll) return VSRK_ERR_UNSUPPORTED;
+    a.qx = qx->ptr;
+    a.qsn = qx->sn;
+    a.qsw = qx->sw;
+    a.xo = xo->ptr;
+    a.osn = xo->sn;
+    a.osw = xo->sw;
+    a.qsh = q->shift;
+    a.qmu = q->mean;
+    a.qis = q->invstd;
+    a.qgm = q->gamma;
+    a.qsdy = q->sum_dy;
+    a.qsdyx = q->sum_dy_xhat;
+    a.qinv_count = (float)(1.0 / q->count);
+  }
   if (mode == 2) {
     const int64_t span_n = 32 * 4 / std::max(a.dhw, 1) + 2;
     if (2 * (span_n * bnx->sn + (int64_t)a.dhw * bnx->sw + bnx->c) >= 0x7FFFFFF0ll) return VSRK_ERR_UNSUPPORTED;
@@ -1242,6 +1361,7 @@ extern "C" int vsrk_conv_fwd_reduce(const vsrk_conv_desc* d, const vsrk_tensor5*
       a.ntiles = ceil_div(a.nvox, 32 * pw_m<NC>());
       grid = std::min(pw_grid(a.ntiles), pw_num_cus());
       if (mode == 1) launch_fwd_reduce<NC, pw_m<NC>(), 1, H>(a, grid, s);
+      else if (q) launch_fwd_reduce<NC, pw_m<NC>(), 2, H, true>(a, grid, s);
       else launch_fwd_reduce<NC, pw_m<NC>(), 2, H>(a, grid, s);
     };
     switch (ncb) {
@@ -1259,6 +1379,25 @@ extern "C" int vsrk_conv_fwd_reduce(const vsrk_conv_desc* d, const vsrk_tensor5*
   pw_red_final_kernel<<<y->c, 256, 0, s>>>(a.red_ws, grid, 32 * ncb, ocpr, 64 / ocpr, y->c, out_a, out_b);
   VSRK_LAUNCH_CHECK("conv_fwd_reduce_final");
   return VSRK_OK;
+}
+
+extern "C" int vsrk_conv_fwd_reduce(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed,
+                                    const float* bias, const float* pro_scale, const float* pro_shift,
+                                    const vsrk_tensor5* y, int32_t mode, const vsrk_tensor5* bnx, const float* scale,
+                                    const float* shift, const float* mean, const float* invstd, float* out_a,
+                                    float* out_b, void* workspace, size_t workspace_bytes, void* stream) {
+  return fwd_reduce_impl(d, x, w_packed, bias, pro_scale, pro_shift, y, mode, bnx, scale, shift, mean, invstd, out_a,
+                         out_b, workspace, workspace_bytes, stream, nullptr, nullptr, nullptr);
+}
+
+extern "C" int vsrk_conv_fwd_reduce_bnb(const vsrk_conv_desc* d, const vsrk_tensor5* bn_x, const vsrk_bn_contrib* pre,
+                                        const vsrk_tensor5* x_out, const void* w_packed, const vsrk_tensor5* y,
+                                        const vsrk_tensor5* bnx, const float* scale, const float* shift,
+                                        const float* mean, const float* invstd, float* out_a, float* out_b,
+                                        void* workspace, size_t workspace_bytes, void* stream) {
+  VSRK_CHECK(bn_x && pre && x_out, "conv_fwd_reduce_bnb: null argument");
+  return fwd_reduce_impl(d, &pre->dz, w_packed, nullptr, nullptr, nullptr, y, 2, bnx, scale, shift, mean, invstd,
+                         out_a, out_b, workspace, workspace_bytes, stream, bn_x, pre, x_out);
 }
 
 namespace {

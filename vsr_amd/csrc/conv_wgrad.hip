@@ -475,7 +475,9 @@ extern "C" size_t vsrk_conv_wgrad_workspace_size(const vsrk_conv_desc* d, const 
   int ns, tps, nt, dzc;
   size_t roll = 0;
   if (!vsrk_wgrad_roll_plan(d, x, dy, &ns, &tps, &nt, &dzc, &roll)) roll = 0;
-  return std::max(std::max(wgrad_plan(d, x, dy).ws_bytes, vsrk_conv_wgrad_pw_workspace(d, x, dy)), roll);
+  VsrkRowPlan rp;
+  const size_t row = vsrk_wgrad_row_plan(d, x, dy, &rp) ? rp.ws_bytes : 0;
+  return std::max(std::max(std::max(wgrad_plan(d, x, dy).ws_bytes, vsrk_conv_wgrad_pw_workspace(d, x, dy)), roll), row);
 }
 
 template <typename T, int NCO, int NCI, int KK, bool VEC>
@@ -527,6 +529,19 @@ extern "C" int vsrk_conv_wgrad(const vsrk_conv_desc* d, const vsrk_tensor5* x, c
         wgrad_reduce_kernel<<<(int)ceil_div64(total, 64), 256, 0, s>>>(
             (const float*)workspace, dw, dbias, 2 * ns, 3 * nci * nco, 9 * 1024 + 32, dy->c, x->c, 3, 3, 3, nco, nci,
             32, 32, std::min(d->pd, 2), perm_r, dy_scale, accumulate);
+      VSRK_LAUNCH_CHECK("conv_wgrad_reduce");
+      return VSRK_OK;
+    }
+  }
+  if (workspace && dy->n * dy->d * dy->h * dy->w > 0) {
+    // rolling-row Conv2d 3x3 kernel (conv_wgrad_row.hip): 32 x 64 channel slabs
+    VsrkRowPlan rp;
+    if (vsrk_conv_wgrad_row(d, x, dy, dbias != nullptr, (float*)workspace, workspace_bytes, &rp, s)) {
+      VSRK_LAUNCH_CHECK("conv_wgrad(row)");
+      const int64_t total = (int64_t)dy->c * x->c * 9 + (dbias ? dy->c : 0);
+      wgrad_reduce_kernel<<<(int)ceil_div64(total, 64), 256, 0, s>>>(
+          (const float*)workspace, dw, dbias, rp.nsplit, rp.ncot * rp.ncic, rp.slab, dy->c, x->c, 1, 3, 3,
+          rp.ncot, rp.ncic, rp.cot_w, 64, 0, perm_r, dy_scale, accumulate);
       VSRK_LAUNCH_CHECK("conv_wgrad_reduce");
       return VSRK_OK;
     }

@@ -280,6 +280,42 @@ def conv_reduce(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, *, bias: tor
     return out
 
 
+def conv_reduce_bnb(bn_x: torch.Tensor, dz: torch.Tensor, pst: torch.Tensor, gamma, pred: torch.Tensor,
+                    count: float, x_out: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, *, bnx: torch.Tensor,
+                    st: torch.Tensor) -> torch.Tensor | None:
+    """conv_reduce's BN+ReLU backward form (a square 1x1x1 data gradient into
+    y, bnx / st the next BatchNorm's) whose input is the BN+ReLU backward
+    apply of the previous BatchNorm, computed in the operand load
+    (vsrk_conv_fwd_reduce_bnb): x_out receives
+    bn_relu_bwd_apply(bn_x, dz, pst, gamma, pred, count) -- bitwise -- for
+    the weight gradient.  y may be dz's storage.  -> (2, C) fp32 sums of y,
+    or None when not eligible (nothing launched: apply + conv_reduce)."""
+    if not FUSE:
+        return None
+    lib = _lib()
+    d = _desc((1, 1, 1), (0, 0, 0), PRO_NONE)
+    c = y.shape[-1]
+    out = torch.empty((2, c), dtype=torch.float32, device=y.device)
+    qv, ov, yv, bv = N.t5(bn_x), N.t5(x_out), N.t5(y), N.t5(bnx)
+    pst, pred = pst.contiguous(), pred.contiguous()
+    g = gamma.contiguous() if gamma is not None else None
+    pre = N.BnContrib(N.t5(dz), 0, pst[0].data_ptr(), pst[1].data_ptr(), pst[2].data_ptr(), pst[3].data_ptr(),
+                      N.ptr(g), pred[0].data_ptr(), pred[1].data_ptr(), float(count))
+    ws = workspace(lib.vsrk_conv_fwd_reduce_workspace(C.byref(d), C.byref(yv)), y.device)
+
+    def launch():
+        return lib.vsrk_conv_fwd_reduce_bnb(C.byref(d), C.byref(qv), C.byref(pre), C.byref(ov), wp.data_ptr(),
+                                            C.byref(yv), C.byref(bv), *(st[i].data_ptr() for i in range(4)),
+                                            out[0].data_ptr(), out[1].data_ptr(), ws.data_ptr(), ws.numel(),
+                                            N.stream_ptr(y.device))
+
+    rc = (timer.wrap(("conv_fwd", (1, 1, 1)), N.t5(dz), yv, launch, _launched) if timer is not None else launch())
+    if rc == 2:  # VSRK_ERR_UNSUPPORTED
+        return None
+    N.check(rc, "conv_fwd_reduce_bnb")
+    return out
+
+
 def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, k, pad, dw: torch.Tensor, dbias: torch.Tensor | None = None, *,
                prologue: int = PRO_NONE, pro_scale: torch.Tensor | None = None,
                pro_shift: torch.Tensor | None = None, dy_scale: float = 1.0, perm_r: int = 1,
@@ -304,7 +340,7 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, k, pad, dw: torch.Tensor, dbia
 
 
 def set_conv_path(path: str, mode: int) -> None:
-    """Select a conv kernel family ("fast", "pw", "roll", "thin", "wgrad_pipe", "wgrad_roll"): -1 default, 0 off, 1 on
+    """Select a conv kernel family ("fast", "pw", "roll", "thin", "wgrad_pipe", "wgrad_roll", "wgrad_row"): -1 default, 0 off, 1 on
     (for "roll" / "wgrad_roll": 1 forces the rolling kernel on every eligible
     shape, the default also skips shallow output depths where it is slower)."""
     N.check(_lib().vsrk_conv_set_path(path.encode(), int(mode)), "conv_set_path")

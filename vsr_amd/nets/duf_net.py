@@ -327,11 +327,16 @@ class DUFNet(BaseNet):
             if work2 is not None:
                 work2.wait()
             dt1 = torch.empty_like(t1)
-            F.bn_relu_bwd_apply(t1, dz2, st2, u.bn2.weight, red2, st2.count, dt1, False)
-            # dz2 is dead: dz1 reuses its storage; bn1's backward reduce comes
-            # out of the data gradient's store pass where the shape allows
+            # dz1 reuses dz2's storage; bn2's backward apply is computed in
+            # conv1's data-gradient operand load (dt1 stored once, for the
+            # weight gradient) and bn1's backward reduce comes out of its
+            # store pass, where the shape allows
             dz1 = dz2
-            pre1 = F.conv_reduce(dt1, F.pack_weight(u.conv1.weight, 1, cd), dz1, bnx=R, st=st1)
+            w1t = F.pack_weight(u.conv1.weight, 1, cd)
+            pre1 = F.conv_reduce_bnb(t1, dz2, st2, u.bn2.weight, red2, st2.count, dt1, w1t, dz1, bnx=R, st=st1)
+            if pre1 is None:
+                F.bn_relu_bwd_apply(t1, dz2, st2, u.bn2.weight, red2, st2.count, dt1, False)
+                pre1 = F.conv_reduce(dt1, w1t, dz1, bnx=R, st=st1)
             if pre1 is None:
                 dgrad(u.conv1, dt1, dz1, K1, P0)
             red1, work1 = self._bn_backward_reduce(u.bn1, R, dz1, st1, grads, red=pre1)
