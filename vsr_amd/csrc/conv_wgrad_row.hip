@@ -263,11 +263,10 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void wgrad_row_kernel(RowArgs a) {
         }
     }
     // 12 groups G = (k-chunk G / 3, kh G % 3): 3 x fragments (+ the k-chunk's
-    // 2 dy fragments at kh 0) and 6 MFMAs; group G + 2's reads are issued
-    // before group G's MFMAs (a register triple buffer: the LDS latency under
-    // load exceeds one group of MFMAs), the scheduler kept from sinking them
-    // to their use.
-    uint4 xf[3][3], yf[2][2];
+    // 2 dy fragments at kh 0) and 6 MFMAs; group G + 1's reads are issued
+    // before group G's MFMAs (a register double buffer; two groups ahead
+    // measured no faster), the scheduler kept from sinking them to their use.
+    uint4 xf[2][3], yf[2][2];
     auto load_group = [&](int G) __attribute__((always_inline)) {
       const int kc = G / 3, kh = G % 3;
       if (kh == 0) {
@@ -275,13 +274,12 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void wgrad_row_kernel(RowArgs a) {
         for (int b = 0; b < 2; ++b) yf[kc & 1][b] = rw_frag(ya[b][0] + kc * 4096, ya[b][1] + kc * 4096);
       }
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) xf[G % 3][kw] = rw_frag(xa[kh][kw][0] + kc * 4096, xa[kh][kw][1] + kc * 4096);
+      for (int kw = 0; kw < 3; ++kw) xf[G & 1][kw] = rw_frag(xa[kh][kw][0] + kc * 4096, xa[kh][kw][1] + kc * 4096);
     };
     load_group(0);
-    load_group(1);
 #pragma unroll
     for (int G = 0; G < 3 * RW_KC; ++G) {
-      if (G + 2 < 3 * RW_KC) load_group(G + 2);
+      if (G + 1 < 3 * RW_KC) load_group(G + 1);
       __builtin_amdgcn_sched_barrier(0);
       if (a.prio) __builtin_amdgcn_s_setprio(1);
       const int kc = G / 3, kh = G % 3;
@@ -289,8 +287,8 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void wgrad_row_kernel(RowArgs a) {
       for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
         for (int b = 0; b < 2; ++b)
-          if (RW_ABL & 2) acc[kh][kw][b][0] += __builtin_bit_cast(float, yf[kc & 1][b].x ^ xf[G % 3][kw].y);
-          else acc[kh][kw][b] = rw_mfma(__builtin_bit_cast(V8, yf[kc & 1][b]), __builtin_bit_cast(V8, xf[G % 3][kw]),
+          if (RW_ABL & 2) acc[kh][kw][b][0] += __builtin_bit_cast(float, yf[kc & 1][b].x ^ xf[G & 1][kw].y);
+          else acc[kh][kw][b] = rw_mfma(__builtin_bit_cast(V8, yf[kc & 1][b]), __builtin_bit_cast(V8, xf[G & 1][kw]),
                                    acc[kh][kw][b]);
       if (kh == 1 && kc == cib) {  // wave-uniform
 #pragma unroll
