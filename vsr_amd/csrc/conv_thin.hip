@@ -658,6 +658,8 @@ int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
                        const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s) {
   if (!thin_enabled()) return 0;
   if (!vsrk_is16(x->dtype)) return 0;
+  if (const int st = vsrk_conv_fwd_stencil(d, x, w_packed, bias, residual, mask, y, s)) return st;
+  if (const int st = vsrk_conv_fwd_stencil_out(d, x, w_packed, bias, residual, mask, y, s)) return st;
   if (x->shuffle > 1 || y->shuffle > 1 || d->bias_perm_r > 1) return 0;
   if ((residual && residual->shuffle > 1) || (mask && mask->shuffle > 1)) return 0;
   const int K = d->kd * d->kh * d->kw * x->c;

@@ -17,6 +17,14 @@ int vsrk_conv_fwd_fast(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
                        const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
 // thin-channel path of vsrk_conv_fwd (conv_thin.hip): cin <= 4 or cout <= 3;
 // same return convention.
+// one-input-channel 3x3 stencil (conv_stencil.hip): 1 = launched, 0 = not eligible, < 0 = -(error status)
+int vsrk_conv_fwd_stencil(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                          const vsrk_tensor5* residual, const vsrk_tensor5* mask, const vsrk_tensor5* y,
+                          hipStream_t s);
+int vsrk_conv_fwd_stencil_out(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed,
+                              const float* bias, const vsrk_tensor5* residual, const vsrk_tensor5* mask,
+                              const vsrk_tensor5* y, hipStream_t s);
+void vsrk_conv_set_stencil_mode(int mode);
 int vsrk_conv_fwd_thin(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                        const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
