@@ -167,6 +167,16 @@ def test_net_matches_golden(name, precision):
             tol = max(3e-2, 3 * fx["fp16_env"][k])
         else:
             tol = max(8e-2, 2 * fx["bf16_env"][k])
+        if precision != "fp32" and k == "tail.conv.bias" and not isinstance(out, list):
+            # the bias of the conv feeding the L1 loss gets sum_v sign(o_v - hr_v) / N:
+            # every residual within the output's own 16-bit error of zero can flip
+            # (2 / N each) for ANY implementation at this precision -- the 16-bit
+            # envelope's draws happened to flip none on some fixtures
+            o64, h64 = _flat(fx["output64"]).double(), _flat(fx["hr"]).double()
+            near = ((o64 - h64).abs() <= d.max().item()).sum().item()
+            ref_b = fx["grad_full64"][k].double().norm().item() if k in fx["grad_full64"] else None
+            if ref_b:
+                tol = max(tol, 2.0 * near / o64.numel() / ref_b)
         assert rel <= tol, (k, rel, tol)
 
 
