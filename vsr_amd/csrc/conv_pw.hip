@@ -1425,14 +1425,19 @@ PwWPlan pw_wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk
   // chunk (VSRK_PW_WGRAD_CI8=1: waves own blocks w and w + 4) read dY once
   // but ran 2.3-2.5 TB/s at 160-224 channels (one workgroup per CU, wave 0
   // holding two blocks of five) against 4.4-4.8 TB/s at <= 128.
+  // Exception, measured (profiles/r4_pw_wgrad_ci8_ab.txt): at 224 channels
+  // the 4 + 3 split's stage (88 KB) keeps one workgroup per CU anyway, and
+  // one chunk of 7 reading dY once is 1568 -> 1071 us (DUF unit 5); at 160
+  // and 192 the split runs two workgroups per CU and stays ahead.
   static int ci8 = -1;
-  if (ci8 < 0) {
+  if (ci8 == -1) {
     const char* e = getenv("VSRK_PW_WGRAD_CI8");
-    ci8 = (e && e[0] == '1') ? 1 : 0;
+    ci8 = !e ? -2 : (e[0] == '1' ? 1 : 0);  // -2: automatic
   }
-  p.ncit = std::min(cib, ci8 ? 8 : 4);
+  const bool one_chunk = ci8 == 1 || (ci8 == -2 && cib == 7);
+  p.ncit = std::min(cib, one_chunk ? 8 : 4);
   p.ci_chunks = ceil_div(cib, p.ncit);
-  if (!ci8) p.ncit = ceil_div(cib, p.ci_chunks);
+  if (!one_chunk) p.ncit = ceil_div(cib, p.ci_chunks);
   if (p.nco < 2) return p;
   p.ncoiw = ceil_div(p.ncit, 4);
   p.nchunks = p.co_chunks * p.ci_chunks;
