@@ -32,6 +32,10 @@ constexpr int ST_CO = 64;                                // output channels (8 l
 constexpr int ST_TASK = ST_TR * ST_TC * (ST_CO / 8) / ST_THR;  // 16 (voxel, chunk) tasks per thread
 
 typedef float st_f2 __attribute__((ext_vector_type(2)));
+typedef uint32_t st_u32x4 __attribute__((ext_vector_type(4)));
+#ifndef ST_NT
+#define ST_NT 1  // non-temporal output stores (tail data gradient 681 -> 591 us); 0 for A/B
+#endif
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x4_t st_mfma(bf16x8 a, bf16x8 b, f32x4_t c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -141,7 +145,11 @@ __global__ __launch_bounds__(ST_THR) void stencil_in_kernel(StArgs a) {
       if (cur.h0 + r < a.H && cur.w0 + c < a.W) {
         H* yp = reinterpret_cast<H*>(a.y) + cur.yo + (int64_t)(cur.h0 + r) * a.ysh + (int64_t)(cur.w0 + c) * a.ysw +
                 8 * c8;
+#if ST_NT
+        __builtin_nontemporal_store(__builtin_bit_cast(st_u32x4, Chunk<H>::pack(o)), reinterpret_cast<st_u32x4*>(yp));
+#else
         *reinterpret_cast<uint4*>(yp) = Chunk<H>::pack(o);
+#endif
       }
     }
     cur = nxt;
