@@ -35,6 +35,9 @@ using namespace vsrk_conv;
 
 constexpr int PW_THR = 256;  // 4 waves, one per SIMD
 constexpr int PW_KP = 64;    // wgrad voxels per stage
+#ifndef PW_NT
+#define PW_NT 2  // non-temporal output stores of the staged kernel (DUF 75.8 -> 75.4 ms, profiles/r4_pw_nt_ab.txt); 0 for A/B
+#endif
 #ifndef PW_BXPRE
 #define PW_BXPRE 1  // fused BN-backward reduce: BN input rows loaded ahead of the MFMAs (0: in the store pass)
 #endif
@@ -517,7 +520,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
         *reinterpret_cast<uint4*>(buf + row * RS + c * 16) = v;
         const uint32_t off = row_off(tb, row, v0, a.osn, a.osw);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), ro,
-                                               (int)(8 * c < a.cin ? off + 16 * c : PW_OOB), 0, 0);
+                                               (int)(8 * c < a.cin ? off + 16 * c : PW_OOB), 0, PW_NT);
       }
     } else {
 #pragma unroll
@@ -642,7 +645,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
           const bool vox_ok = AL || v0 + row < a.nvox;
           if (!(a.ablate & 1))
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), ry,
-                                                   (int)(rch_ok ? off + 2 * (co0 + 8 * rcol) : PW_OOB), 0, 0);
+                                                   (int)(rch_ok ? off + 2 * (co0 + 8 * rcol) : PW_OOB), 0, PW_NT);
           if (vox_ok && rch_ok) {
             float o[8];
             Chunk<H>::unpack(v, o);  // the stored (rounded) values, as the separate pass reads them
@@ -711,7 +714,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
         const uint32_t off = row_off(tb, row, v0, a.ysn, a.ysw);
         if (!(a.ablate & 1))
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), ry,
-                                                 (int)(co0 + c < a.cout ? off + 2 * (co0 + c) : PW_OOB), 0, 0);
+                                                 (int)(co0 + c < a.cout ? off + 2 * (co0 + c) : PW_OOB), 0, PW_NT);
       }
     }
     t = tn;

@@ -42,6 +42,11 @@
 #include <cstdlib>
 #include "conv_common.h"
 
+#ifndef ROLL_NT
+#define ROLL_NT 0  // A/B: non-temporal output stores in the transposed epilogue
+#endif
+typedef uint32_t roll_u32x4 __attribute__((ext_vector_type(4)));
+
 namespace {
 using namespace vsrk_conv;
 
@@ -691,7 +696,11 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) t[e] += o[e];
           }
+#if ROLL_NT
+          __builtin_nontemporal_store(__builtin_bit_cast(roll_u32x4, Chunk<H>::pack(t)), reinterpret_cast<roll_u32x4*>(yp));
+#else
           *reinterpret_cast<uint4*>(yp) = Chunk<H>::pack(t);
+#endif
         }
       }
     }
