@@ -335,7 +335,12 @@ int vsrk_conv_fwd_stencil(const vsrk_conv_desc* d, const vsrk_tensor5* x, const 
   a.ntiles = (int)ntiles;
   a.out_scale = d->out_scale;
   a.relu = d->act == VSRK_ACT_RELU;
-  const int want = (int)vsrk_capped_grid((int64_t)st_num_cus() * 8);
+  static int per_cu = -1;  // workgroups per CU (VSRK_STENCIL_WG A/B: 2 / 4 / 8 / 16 -> 625 / 607 / 587 / 572 us)
+  if (per_cu < 0) {
+    const char* e = getenv("VSRK_STENCIL_WG");
+    per_cu = e ? std::max(1, atoi(e)) : 16;
+  }
+  const int want = (int)vsrk_capped_grid((int64_t)st_num_cus() * per_cu);
   a.tiles_per_blk = (int)ceil_div64(ntiles, want);
   const int grid = (int)ceil_div64(ntiles, a.tiles_per_blk);
   vsrk_dispatch16(x->dtype, [&](auto tag) {
