@@ -26,6 +26,10 @@ CASES = {
     "duf1x1x1_160": (64, 7, 128, 128, 160, 160, (1, 1, 1), (0, 0, 0)),
     "duf1x1x1_192": (64, 5, 128, 128, 192, 192, (1, 1, 1), (0, 0, 0)),
     "duf1x1x1_64": (64, 7, 128, 128, 64, 64, (1, 1, 1), (0, 0, 0)),
+    # DUF's filter / residual head 1x1 convs at depth 1 (duf_net.py:40-49)
+    "duf_fn1": (64, 1, 128, 128, 256, 512, (1, 1, 1), (0, 0, 0)),
+    "duf_fn2": (64, 1, 128, 128, 512, 400, (1, 1, 1), (0, 0, 0)),
+    "duf_rn1": (64, 1, 128, 128, 256, 256, (1, 1, 1), (0, 0, 0)),
     # EDSR tail conv F -> 1 at HR (thin-channel kernels: fwd = thin-out, dgrad = thin-in)
     "tail": (64, 1, 512, 512, 64, 1, (1, 3, 3), (0, 1, 1)),
     "head": (64, 1, 128, 128, 1, 64, (1, 3, 3), (0, 1, 1)),

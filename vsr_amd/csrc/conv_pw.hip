@@ -1428,16 +1428,18 @@ PwWPlan pw_wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk
   // chunk (VSRK_PW_WGRAD_CI8=1: waves own blocks w and w + 4) read dY once
   // but ran 2.3-2.5 TB/s at 160-224 channels (one workgroup per CU, wave 0
   // holding two blocks of five) against 4.4-4.8 TB/s at <= 128.
-  // Exception, measured (profiles/r4_pw_wgrad_ci8_ab.txt): at 224 channels
-  // the 4 + 3 split's stage (88 KB) keeps one workgroup per CU anyway, and
-  // one chunk of 7 reading dY once is 1568 -> 1071 us (DUF unit 5); at 160
-  // and 192 the split runs two workgroups per CU and stays ahead.
+  // Exception, measured (profiles/r4_pw_wgrad_ci8_ab.txt): where the 4-block
+  // split's stage (2 x (nco + 4) x 4 KB) is over 80 KB it keeps one workgroup
+  // per CU anyway, and chunks of up to 8 blocks read dY half as often: DUF
+  // unit 5 (224 -> 224) 1568 -> 1071 us, the heads 256 -> 512 / 512 -> 400 /
+  // 256 -> 256 910 / 1741 / 479 -> 657 / 1169 / 372 us; at 160 and 192
+  // channels the split runs two workgroups per CU and stays ahead.
   static int ci8 = -1;
   if (ci8 == -1) {
     const char* e = getenv("VSRK_PW_WGRAD_CI8");
     ci8 = !e ? -2 : (e[0] == '1' ? 1 : 0);  // -2: automatic
   }
-  const bool one_chunk = ci8 == 1 || (ci8 == -2 && cib == 7);
+  const bool one_chunk = ci8 == 1 || (ci8 == -2 && cib > 4 && std::min(cob, 8) + 4 > 10);
   p.ncit = std::min(cib, one_chunk ? 8 : 4);
   p.ci_chunks = ceil_div(cib, p.ncit);
   if (!one_chunk) p.ncit = ceil_div(cib, p.ci_chunks);
