@@ -1114,6 +1114,17 @@ static bool launch_fwd(const PwArgs& a, int nchunk, bool pro, hipStream_t s) {
   if constexpr (NCB <= 7) {
     if (launch_fwd_staged<NCB, NCB, M, H>(a, grid, nchunk, pro, s)) return true;
   }
+  if constexpr (NCB == 8) {
+    // 256 input channels: the staged kernel in two 128-channel output chunks
+    // per 256 (x read twice, once per chunk, at the staged kernel's rate; the
+    // tile kernel below ran DUF's 256 -> 256 / 512 heads at 1.5-2 TB/s)
+    static int st8 = -1;  // A/B knob VSRK_PW_STAGED8=0
+    if (st8 < 0) {
+      const char* e = getenv("VSRK_PW_STAGED8");
+      st8 = (e && e[0] == '0') ? 0 : 1;
+    }
+    if (st8 && M == 1 && launch_fwd_staged<4, 8, 1, H>(a, grid, 2 * nchunk, pro, s)) return true;
+  }
   if (a.act == VSRK_ACT_PRELU) return false;
   const bool ein = a.has_mask || a.accumulate;
   const size_t lds = (size_t)KS * 2 * COP * 16 + (2 * CIP + COP) * sizeof(float);
