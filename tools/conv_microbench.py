@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--case", default="edsr3x3")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--what", default="fwd,res,wgrad")
+    ap.add_argument("--yf32", action="store_true", help="fp32 forward output (DUF's filter head)")
     ap.add_argument("--paths", default="", help="e.g. k3=0,fast=1 (vsrk_conv_set_path)")
     args = ap.parse_args()
     _native.load()
@@ -64,7 +65,7 @@ def main():
     wt = (torch.randn((co, ci, *k), generator=g) * 0.05).to(dev)
     b = torch.randn(co, generator=g).to(dev)
     do = d + 2 * pad[0] - k[0] + 1
-    y = torch.empty((n, do, h, w, co), dtype=dt if co >= 8 else torch.float32, device=dev)
+    y = torch.empty((n, do, h, w, co), dtype=dt if co >= 8 and not args.yf32 else torch.float32, device=dev)
     res = torch.randn((n, do, h, w, co), generator=g).to(dev, y.dtype)
     gy = _padded(torch.randn((n, do, h, w, co), generator=g), dt)
     dx = torch.empty((n, d, h, w, ci), dtype=dt if ci >= 8 else torch.float32, device=dev)
