@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--what", default="fwd,res,wgrad")
     ap.add_argument("--yf32", action="store_true", help="fp32 forward output (DUF's filter head)")
     ap.add_argument("--paths", default="", help="e.g. k3=0,fast=1 (vsrk_conv_set_path)")
+    ap.add_argument("--stamps", action="store_true",
+                    help="after each case, print the s_memtime stamps of a ROLL_STAMP diagnostic build")
     args = ap.parse_args()
     _native.load()
     for kv in filter(None, args.paths.split(",")):
@@ -117,6 +119,43 @@ def main():
         print(f"{args.case:10s} {name:6s} {ms * 1e3:9.1f} us  {flop / ms / 1e9:8.1f} TFLOP/s  "
               f"({flop / ms / 1e9 / 2500 * 100:.1f}% of 2.5 PF)  "
               f"{nbytes.get(name, 0) / ms / 1e9:7.2f} TB/s (min HBM bytes)", flush=True)
+        if args.stamps:
+            stamp_report(fn)
+
+
+def stamp_report(fn):
+    """Per-step cycle split of waves 0 and 4 (one SIMD) of workgroups 0-15
+    from a conv_roll.hip ROLL_STAMP build: stage wait, barrier, flush
+    (epilogue), compute."""
+    import ctypes
+    import numpy as np
+    lib = _native.load()
+    fn()
+    torch.cuda.synchronize()
+    buf = (ctypes.c_uint * (16 * 2 * 128))()
+    if lib.vsrk_roll_stamps(buf) != 0:
+        raise RuntimeError("vsrk_roll_stamps failed")
+    st = np.frombuffer(buf, dtype=np.uint32).reshape(32, 128).astype(np.int64)
+    names = ["wait", "barrier", "flush", "compute"]
+    tot = np.zeros(4)
+    cnt = 0
+    for w in range(32):
+        s = st[w]
+        if not s.any():
+            continue
+        d = np.diff(s) % (1 << 32)
+        # d[i] = stamp[i+1] - stamp[i]: event (i+1) % 4 ends the phase
+        per = np.zeros(4)
+        for i, v in enumerate(d):
+            per[(i + 1) % 4] += v
+        tot += per
+        cnt += 1
+        if w in (0, 1):
+            print(f"  wg{w // 2} wave{4 * (w % 2)}: " + " ".join(
+                f"{names[(i + 1) % 4][0]}{int(v)}" for i, v in enumerate(d[:40])))
+    if cnt:
+        steps = 127 / 4
+        print("  mean cycles per step: " + "  ".join(f"{n} {tot[i] / cnt / steps:8.0f}" for i, n in enumerate(names)))
 
 
 if __name__ == "__main__":

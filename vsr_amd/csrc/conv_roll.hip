@@ -126,6 +126,8 @@ struct RollGeo {
 // data gradient is (duf_net.py:198-203: bn2 before conv2) fused into the
 // epilogue: per tile and wave, (sum dy', sum dy' xhat) of its 32 channels
 // with dy' = out * (bnx * scale + shift > 0), xhat = (bnx - mean) * invstd
+// (the per-tile partials hold sum dy' (bnx - mean); the final kernel scales
+// by invstd)
 enum { RE_RES = 1, RE_MASK = 2, RE_ACC = 4, RE_RELU = 8, RE_PRELU = 16, RE_PMASK = 32, RE_BNRED = 64 };
 // sub-pixel operand (2-D forms): none, input view, output view
 enum { SP_NONE = 0, SP_X = 1, SP_Y = 2 };
@@ -181,6 +183,16 @@ struct RollArgs {
 };
 
 __device__ __attribute__((aligned(256))) uint4 g_roll_zero[16];
+#ifdef ROLL_STAMP
+// Diagnostic builds only (tools/roll_stamps.py): s_memtime stamps of waves 0
+// and 4 (one SIMD) of workgroups 0-15, kept in VGPR lanes during the walk
+// (no memory operation inside the pipeline) and stored at exit: per step
+// [after the stage wait, after the barrier, after the flush, after compute]
+#ifndef ROLL_STAMP_SKIP
+#define ROLL_STAMP_SKIP 8
+#endif
+__device__ unsigned g_roll_stamp[16 * 2 * 128];
+#endif
 
 template <int N>
 __device__ __forceinline__ void roll_wait_vmcnt() {
@@ -439,10 +451,11 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // ordinary loads (ROLL_PFASM 0) the compiler also waits for them itself
   // before their first use.
   typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-  u32x4_t pre[PREF ? RMS : 1][PREF ? NT : 1][2];
+  typedef u32x4_t PreT[PREF ? RMS : 1][PREF ? NT : 1][2];
+  PreT pre;
   const RView& pv = (EM & RE_RES) ? a.res : a.msk;  // (RE_BNRED: msk is the BN input view)
   const int tv = lane >> 2, tc8 = lane & 3;  // transposed roles: voxel (of 16), 8-channel group
-  auto prefetch = [&](const RTile& tl, int dz) __attribute__((always_inline)) {
+  auto load_pre = [&](PreT& dst, const RTile& tl, int dz) __attribute__((always_inline)) {
     // (ablation 2 issues no DMA, so the compile-time waits would not cover
     // these register loads: never combine them)
     if constexpr (PREF && !(ROLL_ABL & 2)) {
@@ -459,14 +472,15 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
           for (int nt = 0; nt < NT; ++nt) {
             const void* src = ok ? (const void*)(pp + nt * 32) : (const void*)zp;
             if constexpr (ROLL_PFASM)
-              asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(pre[ms][nt][k]) : "v"(src) : "memory");
+              asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst[ms][nt][k]) : "v"(src) : "memory");
             else
-              pre[ms][nt][k] = *reinterpret_cast<const u32x4_t*>(src);
+              dst[ms][nt][k] = *reinterpret_cast<const u32x4_t*>(src);
           }
         }
       }
     }
   };
+  auto prefetch = [&](const RTile& tl, int dz) __attribute__((always_inline)) { load_pre(pre, tl, dz); };
   auto settle = [&]() __attribute__((always_inline)) {
     if constexpr (PREF) {
 #pragma unroll
@@ -578,9 +592,29 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // its flush): a row is parked in two halves of 16 voxels, voxel v in piece
   // (v % 16) / 8, row v % 8 (128 bytes), 16-byte column c at c ^ (v & 7)
   // (conflict-free parking and read-back; 2 KB per wave fits every slot form).
-  auto epilogue_tr = [&](const f32x16 (&A)[RMS], const RTile& tl, int dz, int nt, bool use_pre, char* scr)
+  // Epilogue operand modes: EO_PRE takes the slice's prefetch; EO_LOAD loads
+  // the operand synchronously -- 3-D RE_BNRED: every row's BN input at the
+  // start, so a bank waits for one load latency instead of one
+  // per row, each behind the stores of the rows before it (the tile-end flush
+  // of the banks that were not prefetched: -6 % at DUF's F = 224 unit)
+  enum { EO_LOAD = 0, EO_PRE = 1 };
+  auto epilogue_tr = [&](const f32x16 (&A)[RMS], const RTile& tl, int dz, int nt, int omode, char* scr)
                          __attribute__((always_inline)) {
+    const bool use_pre = omode == EO_PRE;
     char* ws = scr + wave * 1024;
+    // (3-D RE_BNRED: EO_LOAD must not reuse `pre`: at the end of a tile it
+    // may still hold the finishing bank's prefetched operand)
+    PreT pop;
+    if constexpr (PREF && KD == 3) {
+      if (omode == EO_PRE) {
+#pragma unroll
+        for (int ms = 0; ms < RMS; ++ms)
+#pragma unroll
+          for (int k = 0; k < 2; ++k) pop[ms][0][k] = pre[ms][0][k];
+      } else {
+        load_pre(pop, tl, dz);
+      }
+    }
 #pragma unroll
     for (int ms = 0; ms < RMS; ++ms) {
       const int ho = tl.h0 + wave * RMS + ms;
@@ -622,17 +656,18 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
             Chunk<H>::unpack(Chunk<H>::pack(t), tr);  // the stored (rounded) dz, as the separate reduce reads it
             uint4 xv;
             if constexpr (PREF) {
-              if (use_pre) xv = __builtin_bit_cast(uint4, pre[ms][nt][k]);
-              else xv = *reinterpret_cast<const uint4*>(reinterpret_cast<const H*>(a.bnx) +
-                                                        (yp - reinterpret_cast<H*>(a.y.ptr)));
+              xv = __builtin_bit_cast(uint4, pop[ms][nt][k]);
             } else {
               xv = *reinterpret_cast<const uint4*>(reinterpret_cast<const H*>(a.bnx) +
                                                    (yp - reinterpret_cast<H*>(a.y.ptr)));
             }
             Chunk<H>::unpack(xv, xb);
-            float cst[4][8];  // scale, shift, mean, invstd of the lane's 8 channels
+            // scale, shift, mean of the lane's 8 channels (the sums of
+            // dy' (x - mean) take invstd in the final kernel: one VALU op
+            // and two LDS reads less per element chunk)
+            float cst[3][8];
 #pragma unroll
-            for (int k4 = 0; k4 < 4; ++k4) {
+            for (int k4 = 0; k4 < 3; ++k4) {
               const float4 c0 = *reinterpret_cast<const float4*>(lbn + k4 * a.cout_pad + co);
               const float4 c1 = *reinterpret_cast<const float4*>(lbn + k4 * a.cout_pad + co + 4);
               cst[k4][0] = c0.x; cst[k4][1] = c0.y; cst[k4][2] = c0.z; cst[k4][3] = c0.w;
@@ -642,7 +677,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
             for (int e = 0; e < 8; ++e) {
               const float dy = fmaf(xb[e], cst[0][e], cst[1][e]) > 0.f ? tr[e] : 0.f;
               rs1[e] += dy;
-              rs2[e] = fmaf(dy, (xb[e] - cst[2][e]) * cst[3][e], rs2[e]);
+              rs2[e] = fmaf(dy, xb[e] - cst[2][e], rs2[e]);
             }
           }
           if constexpr (EM & RE_MASK) {
@@ -718,7 +753,8 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       for (int b = 0; b < 3; ++b) {
         if (all || b == bdone) {
           const int dz = P - (P + 3 - b) % 3;  // the output depth in bank b
-          if (!(ROLL_ABL & 4) && dz >= tl.z0 && dz < tl.z1) epilogue_tr(acc[b], tl, dz, 0, use_pre && b == bdone, scr);
+          if (!(ROLL_ABL & 4) && dz >= tl.z0 && dz < tl.z1)
+            epilogue_tr(acc[b], tl, dz, 0, (use_pre && b == bdone) ? EO_PRE : EO_LOAD, scr);
 #pragma unroll
           for (int m = 0; m < RMS; ++m)
 #pragma unroll
@@ -752,7 +788,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     } else {
 #pragma unroll
       for (int b = 0; b < NACC; ++b) {
-        if (!(ROLL_ABL & 4) && P >= tl.z0 && P < tl.z1) epilogue_tr(acc[b], tl, P, b, use_pre, scr);
+        if (!(ROLL_ABL & 4) && P >= tl.z0 && P < tl.z1) epilogue_tr(acc[b], tl, P, b, use_pre ? EO_PRE : EO_LOAD, scr);
 #pragma unroll
         for (int m = 0; m < RMS; ++m)
 #pragma unroll
@@ -761,6 +797,20 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     }
   };
   // compute walk: tile ct (decoded when the walk enters it), slice cs, chunk cc
+#ifdef ROLL_STAMP
+  unsigned stv0 = 0, stv1 = 0;
+  int stc = -4 * ROLL_STAMP_SKIP;
+  auto stamp = [&]() __attribute__((always_inline)) {
+    if (stc >= 0 && stc < 128) {
+      const unsigned tv = (unsigned)__builtin_amdgcn_s_memtime();
+      if (stc < 64) stv0 = lane == stc ? tv : stv0;
+      else stv1 = lane == stc - 64 ? tv : stv1;
+    }
+    ++stc;
+  };
+#else
+  auto stamp = [&]() __attribute__((always_inline)) {};
+#endif
   int t = t_lo + jb;
   if (t >= t_hi) {
     if constexpr (EM & RE_PMASK) a.slope_ws[(blockIdx.x * RNW + wave) * 64 + lane] = 0.f;
@@ -838,8 +888,10 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       if (ROLL_LEAN || tnext) roll_wait_vmcnt<RNQ>();  // this stage landed (and any earlier prefetch); the next stays in flight
       else roll_wait_vmcnt<0>();
     }
+    stamp();
     if constexpr (ROLL_ABL & 16) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // this slot ready, the previous one free
+    stamp();
     // WR: the compute walk entered a tile of another output block.  Every
     // wave is past the last stage that read the old image (the barrier
     // above), so the new one is issued now, its latency covered by the flush,
@@ -856,6 +908,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       if (ppre) settle();
       flush(ptl, pdi, pall, ppre, lds + ((decltype(slot_c)::value + 2) % 3) * RSLOT);
     }
+    stamp();
     if (WR && wreload) {
       roll_wait_vmcnt<0>();
       asm volatile("s_barrier" ::: "memory");
@@ -887,6 +940,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       tk1 = a.sptap[(ct.n0 >> 5) + 1];
     }
     compute(slot_c, di + a.pd, kd_mask(ct.z0, ct.z1, di), dn, vn, tnext, tc, tm, tk0, tk1, cc);
+    stamp();
     if constexpr (PREF) {
       if (pf_next) {
         prefetch(ct, pz);
@@ -924,6 +978,13 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   if (ppre) settle();
   flush(ptl, pdi, true, ppre, fscr);
   if constexpr (EM & RE_PMASK) a.slope_ws[(blockIdx.x * RNW + wave) * 64 + lane] = sacc;
+#ifdef ROLL_STAMP
+  if (blockIdx.x < 16 && (wave == 0 || wave == 4)) {
+    unsigned* o = g_roll_stamp + (blockIdx.x * 2 + (wave >> 2)) * 128;
+    o[lane] = stv0;
+    o[64 + lane] = stv1;
+  }
+#endif
 }
 
 // Channel c of the fused BN+ReLU backward reduce: the (tile, wave) partials
@@ -931,8 +992,8 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
 // fixed order, in double.  A (tile, wave) record is [sum: 32 | sum xhat: 32]
 // over the block's channels.
 __global__ __launch_bounds__(256) void roll_bnred_final_kernel(const float* __restrict__ ws, int ntiles, int ntn,
-                                                               int cout, float* __restrict__ o1,
-                                                               float* __restrict__ o2) {
+                                                               int cout, const float* __restrict__ invstd,
+                                                               float* __restrict__ o1, float* __restrict__ o2) {
   const int c = blockIdx.x;
   if (c >= cout) return;
   const int blk = c >> 5, cc = c & 31;
@@ -972,7 +1033,7 @@ __global__ __launch_bounds__(256) void roll_bnred_final_kernel(const float* __re
   }
   if (threadIdx.x == 0) {
     o1[c] = (float)r1[0];
-    o2[c] = (float)r2[0];
+    o2[c] = (float)(r2[0] * (double)invstd[c]);  // the partials are sums of dy' (x - mean)
   }
 }
 
@@ -1305,6 +1366,12 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   return rc == VSRK_OK ? 1 : -rc;
 }
 
+#ifdef ROLL_STAMP
+extern "C" int vsrk_roll_stamps(unsigned* dst) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_roll_stamp), sizeof(g_roll_stamp)) == hipSuccess ? 0 : 1;
+}
+#endif
+
 extern "C" size_t vsrk_conv_prelu_bwd_workspace(void) { return vsrk_roll_slope_ws_floats() * sizeof(float); }
 
 extern "C" int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed,
@@ -1326,7 +1393,7 @@ extern "C" int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* d, const vsrk_tenso
 }
 
 int vsrk_roll_bnred_final(const vsrk_roll_bnred& r, int cout, float* sum_dy, float* sum_dy_xhat, hipStream_t s) {
-  roll_bnred_final_kernel<<<cout, 256, 0, s>>>(r.ws, r.ntiles, r.ntn, cout, sum_dy, sum_dy_xhat);
+  roll_bnred_final_kernel<<<cout, 256, 0, s>>>(r.ws, r.ntiles, r.ntn, cout, r.invstd, sum_dy, sum_dy_xhat);
   VSRK_LAUNCH_CHECK("conv_fwd_reduce(roll) final");
   return VSRK_OK;
 }

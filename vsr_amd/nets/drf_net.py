@@ -38,7 +38,11 @@ epilogue):
     stream, overlapping the data-gradient chain of the frames still to go;
     the runs accumulate in a fixed order (deterministic).  K keeps every
     view's element offsets within 32 bits (7 at cfg 3), so the pipelined
-    kernels stay eligible.  VSR_DRF_SEQ_WGRAD=0: one launch per frame.
+    kernels stay eligible.  The backward's own sequence buffers are
+    allocated in chunks of Kg frames and dropped as soon as every run over a
+    chunk is launched: Kg keeps them within VSR_DRF_SEQ_BUDGET_GB (default
+    16 GiB; at cfg 3 one frame of them is ~1.2 GB, so Kg = 13 instead of all
+    30 frames, ~37 GB).  VSR_DRF_SEQ_WGRAD=0: one launch per frame.
 """
 from __future__ import annotations
 
@@ -317,16 +321,36 @@ class _DRFBase(BaseNet):
         T = len(recs)
         seq = self.SEQ_WGRAD
         seqs: dict = {}
+        # Sequence buffers come in chunks of Kg frames ([r Kg, (r+1) Kg)),
+        # each dropped once every run over its frames is launched (the side
+        # stream keeps the storage alive through record_stream): the extra
+        # memory over per-frame buffers is at most VSR_DRF_SEQ_BUDGET_GB
+        # (default 16) instead of T frames of every buffer (~37 GB at cfg 3).
+        Kg = T
+        if seq:
+            HH0, WW0 = recs[0]["tail_in"].shape[2], recs[0]["tail_in"].shape[3]
+            fe = HH0 * WW0 * f  # dup{len(ups)}
+            hh0, ww0 = HH0, WW0
+            for _, st_ in reversed(self._ups()):
+                hh0, ww0 = hh0 // st_, ww0 // st_
+                fe += hh0 * ww0 * f  # dup{j}
+            fe += (2 * G + 2) * h * w * f + h * w * 4 * f  # gout, gl*, dt1_*, g0, gin, du_u1
+            fe += (2 * G - 1) * H * W * f  # gh*, dt2_*
+            frame_bytes = fe * b * torch.empty((), dtype=cd).element_size()
+            budget = float(os.environ.get("VSR_DRF_SEQ_BUDGET_GB", "16")) * 2 ** 30
+            Kg = max(1, min(T, int(budget // max(frame_bytes, 1))))
+        self._seq_run_frames = Kg  # (tests / bench records)
 
         def sbuf(name, t, hh, ww, c):
             """frame t of a backward sequence buffer (an output gradient a
             weight gradient reads); per-frame buffers without SEQ_WGRAD"""
             if not seq:
                 return new(hh, ww, c)
-            big = seqs.get(name)
+            r = t // Kg
+            big = seqs.get((name, r))
             if big is None:
-                big = seqs[name] = torch.empty((T, b, hh, ww, c), dtype=cd, device=dev)
-            return big[t].unsqueeze(1)
+                big = seqs[(name, r)] = torch.empty((min(Kg, T - r * Kg), b, hh, ww, c), dtype=cd, device=dev)
+            return big[t - r * Kg].unsqueeze(1)
 
         # deferred weight gradients: key -> (param, launch(x, dy, accumulate),
         # {frame: (x, dy)}, runs launched, frames per run K)
@@ -334,9 +358,13 @@ class _DRFBase(BaseNet):
 
         def run_frames(x, dy) -> int:
             """K for a weight: the run's view must keep 32-bit element offsets
-            (B x the frame's span of the wider operand, per frame)"""
+            (B x the frame's span of the wider operand, per frame), and runs
+            must not cross a sequence-buffer chunk (K divides Kg)"""
             span = max(v.stride(0) * b for v in (x, dy))
-            return max(1, min(T, (2 ** 31 - 1) // max(span, 1) - 1))
+            k_ = max(1, min(Kg, (2 ** 31 - 1) // max(span, 1) - 1))
+            while Kg % k_:
+                k_ -= 1
+            return k_
 
         def launch_runs(t):
             """frame t just finished: launch every deferred weight gradient
@@ -361,6 +389,9 @@ class _DRFBase(BaseNet):
                 for u in range(t, t1):
                     del frs[u]
                 pend[key] = (prm, launch, frs, nrun, K)
+            if t % Kg == 0:  # every run over chunk t // Kg is launched: drop its buffers
+                for key in [k_ for k_ in seqs if k_[1] == t // Kg]:
+                    del seqs[key]
 
         def gbuf(prm):
             key = id(prm)
