@@ -254,6 +254,37 @@ def comm_report(net, sync, dev, iters=20):
     return out
 
 
+def metric_report(net, x, y, dev, iters=10):
+    """The reference's per-step metric computation (base_trainer.py:135:
+    _compute_metrics = denormalize (utils.py:1-20) then PSNR / SSIM,
+    metrics.py:20-36, 86-113) on the step's outputs, through the trainer
+    mirror's _metric (one fused HIP kernel each), timed on its own after the
+    timed train steps -- SURVEY 8(d): metrics excluded from the voxels/s
+    figure and reported separately."""
+    from vsr_amd import metrics as M
+    from vsr_amd.runner.trainers import _metric
+    with torch.no_grad():
+        out = net(x)
+    outs = out if isinstance(out, list) else [out]
+    tgts = y if isinstance(y, list) else [y]
+    res = {}
+    for name, fn in (("psnr", M.PSNR()), ("ssim", M.SSIM())):
+        def run():
+            return torch.stack([_metric(fn, o, t, DATASET if DATASET != "mixed" else "acdc")
+                                for o, t in zip(outs, tgts)]).mean()
+        run()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for _ in range(iters):
+            v = run()
+        ev1.record()
+        torch.cuda.synchronize()
+        res[name] = {"ms_per_step": ev0.elapsed_time(ev1) / iters, "value": float(v.item())}
+    res["ms_per_step"] = res["psnr"]["ms_per_step"] + res["ssim"]["ms_per_step"]
+    res["note"] = "denormalize + PSNR + SSIM of the step's outputs, per train step, outside the timed region"
+    return res
+
+
 def run_model(name, args, world, rank, dev):
     spec = MODELS[name]
     torch.manual_seed(0)  # identical initial weights on every rank
@@ -345,6 +376,7 @@ def run_model(name, args, world, rank, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     comm = comm_report(net, sync, dev) if world > 1 else None
+    metrics = metric_report(net, x, y, dev)
     vox_step = B * T * H * W
     peak = PEAK[args.precision]
     achieved = flop / kernel_s if kernel_s > 0 else None
@@ -366,6 +398,7 @@ def run_model(name, args, world, rank, dev):
     }
     if comm is not None:
         res["comm"] = comm
+    res["metrics"] = metrics
     del net, opt, sync
     torch.cuda.empty_cache()
     return res

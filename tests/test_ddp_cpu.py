@@ -124,3 +124,19 @@ def test_syncbn_global_count_uneven_gloo():
         p.join(30)
         assert p.exitcode == 0
     assert got == {0: 4.0, 1: 4.0}
+
+
+def test_scaled_work_divides_once_in_double():
+    """the SyncBN backward sums are divided by the global count,
+    formed in double, exactly once however often wait() is called."""
+    from vsr_amd.nets.duf_net import _ScaledWork
+
+    class _Done:
+        def wait(self):
+            pass
+
+    red = torch.tensor([[3.0, 6.0], [9.0, 12.0]])
+    w = _ScaledWork(_Done(), red, torch.tensor(3.0, dtype=torch.float64), 1.0 / 3.0)
+    w.wait()
+    w.wait()
+    assert torch.equal(red, torch.tensor([[3.0, 6.0], [9.0, 12.0]]) / torch.tensor(1.0))

@@ -64,6 +64,8 @@ import hashlib
 import pytest
 import torch
 
+from vsr_amd import functional as F
+
 from tests.conftest import load_golden
 from vsr_amd import nets
 
@@ -169,15 +171,46 @@ def test_net_matches_golden(name, precision):
             tol = max(8e-2, 2 * fx["bf16_env"][k])
         if precision != "fp32" and k == "tail.conv.bias" and not isinstance(out, list):
             # the bias of the conv feeding the L1 loss gets sum_v sign(o_v - hr_v) / N:
-            # every residual within the output's own 16-bit error of zero can flip
+            # a residual within the output's own 16-bit error of zero can flip
             # (2 / N each) for ANY implementation at this precision -- the 16-bit
-            # envelope's draws happened to flip none on some fixtures
+            # envelope's draws happened to flip none on some fixtures.  Only the
+            # residuals that DID flip in this run widen the bound, by exactly
+            # their 2 / N each (not every residual within the run's
+            # global max error), and never by more than the residuals within
+            # the precision's ALLOWED output error (asserted above) could flip;
+            # the run with the 16-bit stencil tail off must meet the plain bound
+            # (test_tail_bias_without_stencil_meets_envelope)
             o64, h64 = _flat(fx["output64"]).double(), _flat(fx["hr"]).double()
-            near = ((o64 - h64).abs() <= d.max().item()).sum().item()
+            flips = ((got - h64).sign() != (o64 - h64).sign()).sum().item()
+            allowed = 5e-3 if precision == "fp16" else 3e-2
+            near = ((o64 - h64).abs() <= allowed).sum().item()
             ref_b = fx["grad_full64"][k].double().norm().item() if k in fx["grad_full64"] else None
             if ref_b:
-                tol = max(tol, 2.0 * near / o64.numel() / ref_b)
+                tol += 2.0 * min(flips, near) / o64.numel() / ref_b
         assert rel <= tol, (k, rel, tol)
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+@pytest.mark.parametrize("name", [c for c in CASES if c.startswith("edsr")])
+def test_tail_bias_without_stencil_meets_envelope(name, precision):
+    """The EDSR tail bias gradient with the one-channel stencil tail kernels
+    off (the tile kernels round every residual as round 3 did) stays within the
+    16-bit envelope with no sign-flip allowance."""
+    fx = load_golden(name)
+    F.set_conv_path("stencil", 0)
+    try:
+        net = _build(fx, precision)
+        lr, hr = _to(fx["lr"]), _to(fx["hr"])
+        out = net(lr)
+        _l1(out, hr).backward()
+        torch.cuda.synchronize()
+    finally:
+        F.set_conv_path("stencil", -1)
+    k = "tail.conv.bias"
+    g = dict(net.named_parameters())[k].grad.detach().cpu().double()
+    tol = max(3e-2, 3 * fx["fp16_env"][k]) if precision == "fp16" else max(8e-2, 2 * fx["bf16_env"][k])
+    rel = _rel(g, fx, k)
+    assert rel <= tol, (k, rel, tol)
 
 
 def test_cond_fixtures_are_well_conditioned():

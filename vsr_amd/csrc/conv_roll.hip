@@ -620,9 +620,16 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       const int ho = tl.h0 + wave * RMS + ms;
       if (ho >= a.y.h) continue;  // wave-uniform
       const int co = tl.n0 + nt * 32 + 8 * tc8;
-      const float4 b0 = *reinterpret_cast<const float4*>(lbias + co);
-      const float4 b1 = *reinterpret_cast<const float4*>(lbias + co + 4);
-      const float bsv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      // (RE_BNRED: a data gradient, no bias and unit scale -- the host
+      // checks -- so the bias table is not read and the scale not applied)
+      constexpr bool PLAIN = (EM & RE_BNRED) != 0;
+      float bsv[8];
+      if constexpr (!PLAIN) {
+        const float4 b0 = *reinterpret_cast<const float4*>(lbias + co);
+        const float4 b1 = *reinterpret_cast<const float4*>(lbias + co + 4);
+        bsv[0] = b0.x; bsv[1] = b0.y; bsv[2] = b0.z; bsv[3] = b0.w;
+        bsv[4] = b1.x; bsv[5] = b1.y; bsv[6] = b1.z; bsv[7] = b1.w;
+      }
       if constexpr (!PARK2) {
 #pragma unroll
         for (int g = 0; g < 4; ++g)
@@ -644,7 +651,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
         float t[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          t[e] = fmaf(t[e], osc, bsv[e]);
+          if constexpr (!PLAIN) t[e] = fmaf(t[e], osc, bsv[e]);
           if constexpr (EM & RE_RELU) t[e] = fmaxf(t[e], 0.f);
           if constexpr (EM & RE_PRELU) t[e] = t[e] > 0.f ? t[e] : pslope * t[e];
         }
@@ -1152,7 +1159,8 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   if (g_roll_mode == 2 && k3 && y->d == 1 && !bnred && vsrk_g_roll_dz == 0) return 0;
   if (bnred) {
     const vsrk_tensor5* b = bnred->bnx;
-    if (!k3 || d->prologue || d->act != VSRK_ACT_NONE || !b || b->dtype != y->dtype || b->shuffle > 1 ||
+    if (!k3 || d->prologue || d->act != VSRK_ACT_NONE || bias || d->out_scale != 1.f || !b || b->dtype != y->dtype ||
+        b->shuffle > 1 ||
         b->n != y->n || b->d != y->d || b->h != y->h || b->w != y->w || b->c != y->c || b->sn != y->sn ||
         b->sd != y->sd || b->sh != y->sh || b->sw != y->sw)
       return 0;

@@ -45,6 +45,30 @@ __global__ __launch_bounds__(256) void peak_copy_kernel(const uint4* __restrict_
   }
 }
 
+// Block-contiguous form: each workgroup copies one contiguous chunk of
+// 256 x U x 16 bytes, U loads in flight per lane before the stores; non-
+// temporal loads and stores (each byte is touched once).  The grid covers the
+// whole buffer (no grid-stride loop).  Round 5, 2 GiB copy, best of 10, read
+// + write bytes: U = 4 6.22-6.30 TB/s (MI355X_MICROARCH.md: 6.29 measured),
+// U = 8 4.2-4.3, the grid-stride peak_copy_kernel (PEAK_COPY 0) 4.7.
+typedef uint32_t pk_u32x4 __attribute__((ext_vector_type(4)));
+template <int U>
+__global__ __launch_bounds__(256) void peak_copy_chunk_kernel(const pk_u32x4* __restrict__ src,
+                                                              pk_u32x4* __restrict__ dst, int64_t n) {
+  const int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+  pk_u32x4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * 256;
+    if (i < n) v[u] = __builtin_nontemporal_load(src + i);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = base + u * 256;
+    if (i < n) __builtin_nontemporal_store(v[u], dst + i);
+  }
+}
+
 int num_cus() {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
@@ -68,10 +92,22 @@ extern "C" int vsrk_peak_mfma(int32_t iters, float* out, void* stream) {
 
 extern "C" int vsrk_peak_copy(const void* src, void* dst, int64_t bytes, void* stream) {
   VSRK_CHECK(src && dst && bytes > 0 && bytes % 16 == 0, "peak_copy: bad argument");
-  const int blocks = 8 * num_cus();
-  VSRK_CHECK(blocks > 0, "peak_copy: no device");
-  peak_copy_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(reinterpret_cast<const uint4*>(src),
-                                                           reinterpret_cast<uint4*>(dst), bytes / 16);
+  const int64_t n = bytes / 16;
+#ifndef PEAK_COPY
+#define PEAK_COPY 1
+#endif
+  if (PEAK_COPY == 0) {
+    const int blocks = 8 * num_cus();
+    VSRK_CHECK(blocks > 0, "peak_copy: no device");
+    peak_copy_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(reinterpret_cast<const uint4*>(src),
+                                                             reinterpret_cast<uint4*>(dst), n);
+  } else {
+    constexpr int U = PEAK_COPY == 1 ? 4 : 8;
+    const int64_t blocks = (n + 256 * U - 1) / (256 * U);
+    VSRK_CHECK(blocks < (1ll << 31), "peak_copy: buffer too large");
+    peak_copy_chunk_kernel<U><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(
+        reinterpret_cast<const pk_u32x4*>(src), reinterpret_cast<pk_u32x4*>(dst), n);
+  }
   VSRK_LAUNCH_CHECK("peak_copy");
   return VSRK_OK;
 }

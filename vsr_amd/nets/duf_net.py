@@ -66,14 +66,20 @@ class _DenseLayer(nn.Module):
 class _ScaledWork:
     """A SyncBN backward all-reduce in flight: wait() orders the stream after
     it and then divides the summed (sum_dy, sum_dy_xhat) by the global count
-    on the device, so the apply runs with count 1."""
+    on the device, so the apply runs with count 1.  The divisor is formed in
+    double (the count is a device float64, as the single-process path's
+    qinv_count) and rounded once; a second wait() does nothing."""
 
     def __init__(self, work, red, count_dev, mult):
         self.work, self.red, self.count_dev, self.mult = work, red, count_dev, mult
+        self.done = False
 
     def wait(self):
+        if self.done:
+            return
+        self.done = True
         self.work.wait()
-        self.red.div_(self.count_dev.to(torch.float32) * self.mult)
+        self.red.div_((self.count_dev.to(torch.float64) * self.mult).to(self.red.dtype))
 
 
 class DUFNet(BaseNet):
