@@ -232,6 +232,16 @@ int vsrk_prelu_bwd(const vsrk_tensor5* y, const vsrk_tensor5* dy, const vsrk_ten
                    const vsrk_tensor5* dx, float* da, int32_t accumulate_da, void* workspace, size_t workspace_bytes,
                    void* stream);
 
+/* nn.PReLU backward from the layer INPUT x (the pre-activation, what
+ * nn.PReLU itself saves; replaces drf_net.py:55-58,66,83-100's PReLU
+ * autograd for ANY slope, a <= 0 included): dx = (dy [+ dy2]) * (x > 0 ? 1 :
+ * a) and da [+]= sum_{x<0} (dy [+ dy2]) * x.  vsrk_prelu_bwd's output-based
+ * form reads x < 0 as y < 0, exact only while a > 0 (it returns a NaN slope
+ * gradient for a <= 0).  Same views, workspace and determinism. */
+int vsrk_prelu_bwd_pre(const vsrk_tensor5* x, const vsrk_tensor5* dy, const vsrk_tensor5* dy2, const float* a,
+                       const vsrk_tensor5* dx, float* da, int32_t accumulate_da, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
 /* Layout/dtype moves between torch's NC(D)HW fp32 tensors and channels-last
  * views: src is (n, c, d, h, w) fp32 contiguous; channels beyond c in dst are
  * zero-filled (input padding for the 1-channel head convs). */

@@ -159,6 +159,7 @@ def _vs_oracle(precision, lr, hr, dataset, omax, omean, gworst, gmed, rtol):
         rels[k] = (g_m[k] - gr).norm().item() / gr.norm().item()
     worst = max(rels.items(), key=lambda kv: kv[1])
     med = sorted(rels.values())[len(rels) // 2]
+    print("output max / mean", d.max().item(), d.mean().item(), "worst / median gradient", worst, med)
     assert worst[1] <= gworst and med <= gmed, (worst, med)
     rm, rr = _running(mine), _running(ref)
     for k, v in rr.items():
@@ -176,4 +177,4 @@ def test_cfg5_fp16_duf_train_full_batch():
 def test_cfg4_duf_full_volumes_train():
     # bench.py cfg4: two uncropped 30-frame volumes of 64 x 64 LR (256 x 256 HR)
     lr, hr = synth_cine(2, 30, 64, 64, R, "acdc", seed=44, device=DEV)
-    _vs_oracle("bf16", lr, hr, "acdc", 3e-2, 3e-3, 0.1, 3e-2, 2e-2)
+    _vs_oracle("bf16", lr, hr, "acdc", 3e-2, 3e-3, 5e-2, 3e-2, 2e-2)

@@ -10,12 +10,12 @@ and inputs, and compares the output, the PSNR of the denormalised output
 
   * cfg 3 -- DSB15 VSR, DRF (drf_net.py:38-49) at B = 4, T = 30 frames of
     128 x 128, bf16, with the weight gradients on the side stream (the bench
-    setting).  The loss covers sample 0 only, so the oracle runs that one
-    sequence while the HIP kernels run the whole B = 4 grid.
-    Bounds (bf16 storage, 30-step recurrence): output max |d| <= 5e-2, mean
-    <= 3e-3; gradients rel-L2 worst <= 0.1, median <= 3e-2; the scalar PReLU
-    slopes (sums of cancelling terms over 30 frames) |d| <= 0.1 x the largest
-    slope gradient.
+    setting).  The loss covers all four samples; the oracle runs them one
+    sequence at a time (no sample coupling in DRF) and accumulates.
+    Bounds (SURVEY 8(d) bf16): output max |d| <= 3e-2, mean <= 3e-3;
+    gradients rel-L2 worst <= 5e-2, median <= 3e-2; the scalar PReLU slopes
+    (sums of cancelling terms over 30 frames) |d| <= 5e-2 x the largest slope
+    gradient.
   * cfg 5 -- mixed ACDC + DSB15 (half the volumes each, per-volume
     normalisation constants), fp16, batch 8 per GPU: EDSR on 128 slices, DUF
     on 128 seven-frame windows (loss on the first 16 samples, oracle on
@@ -68,6 +68,7 @@ def _compare(mine, ref, out, rout, y, dataset, omax, omean, gworst, gmed, sworst
         rels[k] = (g_m[k] - gr).norm().item() / gr.norm().item()
     worst = max(rels.items(), key=lambda kv: kv[1])
     med = sorted(rels.values())[len(rels) // 2]
+    print("output max / mean", d.max().item(), d.mean().item(), "worst / median gradient", worst, med)
     assert worst[1] <= gworst and med <= gmed, (worst, med)
     return worst, med
 
@@ -90,14 +91,21 @@ def test_cfg3_drf_t30_bf16():
     x = [lr[:, t:t + 1] for t in range(T)]
     y = [hr[:, t:t + 1] for t in range(T)]
     outs = mine(x)
-    torch.stack([Fn.l1_loss(o[:1], t[:1]) for o, t in zip(outs, y)]).mean().backward()
+    torch.stack([Fn.l1_loss(o, t) for o, t in zip(outs, y)]).mean().backward()
+    # the oracle one sequence at a time (DRF couples no samples): the loss over
+    # all B samples is the mean of the per-sample losses, so each run's
+    # backward carries 1 / B and the gradients accumulate
+    routs = []
     with torch.backends.cudnn.flags(enabled=False):
-        routs = ref([v[:1] for v in x])
-        torch.stack([Fn.l1_loss(o, t[:1]) for o, t in zip(routs, y)]).mean().backward()
+        for i in range(B):
+            ro = ref([v[i:i + 1] for v in x])
+            (torch.stack([Fn.l1_loss(o, t[i:i + 1]) for o, t in zip(ro, y)]).mean() / B).backward()
+            routs.append(torch.stack([o.detach() for o in ro]))
     torch.cuda.synchronize()
-    out = torch.stack([o[:1] for o in outs])
-    rout = torch.stack(routs)
-    _compare(mine, ref, out, rout, torch.stack([t[:1] for t in y]), "dsb15", 5e-2, 3e-3, 0.1, 3e-2)
+    out = torch.stack(outs)
+    rout = torch.cat(routs, dim=1)
+    stats = _compare(mine, ref, out, rout, torch.stack(y), "dsb15", 3e-2, 3e-3, 5e-2, 3e-2, sworst=5e-2)
+    print("cfg3 drf worst / median gradient", stats)
 
 
 def _mixed(B, T, H, W, seed):

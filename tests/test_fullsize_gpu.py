@@ -17,7 +17,7 @@ through the HIP path (bf16) against the oracle restatement (oracle/cpu_nets,
 the reference's algorithm, bitwise-pinned to it) run in fp32 on the same
 device with the same weights and inputs: output max |d| <= 3e-2 and mean
 <= 3e-3 (SURVEY §8d bf16 bound), PSNR within 0.01 dB, parameter gradients
-within the bf16 storage envelope (rel-L2 <= 0.1 per parameter, median <= 3e-2).
+within the bf16 storage envelope (rel-L2 <= 5e-2 per parameter, median <= 3e-2).
 """
 import pytest
 import torch
@@ -161,7 +161,8 @@ def test_fullsize_train_step_vs_oracle(model):
         rels[k] = (g_m[k] - gr).norm().item() / gr.norm().item()
     worst = max(rels.items(), key=lambda kv: kv[1])
     med = sorted(rels.values())[len(rels) // 2]
-    assert worst[1] <= 0.1 and med <= 3e-2, (worst, med)
+    print(model, "output max / mean", d.max().item(), d.mean().item(), "worst / median gradient", worst, med)
+    assert worst[1] <= 5e-2 and med <= 3e-2, (worst, med)
     if model == "duf":  # BatchNorm running statistics after the step
         for k, v in ref.state_dict().items():
             if "running" in k:

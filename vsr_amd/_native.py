@@ -125,6 +125,7 @@ _SIGS = {
     "vsrk_prelu_workspace_size": (C.c_size_t, []),
     "vsrk_prelu_wgrad": (C.c_int, [_T5, _T5, _P, _P, C.c_int32, _P, C.c_size_t, _P]),
     "vsrk_prelu_bwd": (C.c_int, [_T5, _T5, _T5, _P, _T5, _P, C.c_int32, _P, C.c_size_t, _P]),
+    "vsrk_prelu_bwd_pre": (C.c_int, [_T5, _T5, _T5, _P, _T5, _P, C.c_int32, _P, C.c_size_t, _P]),
     "vsrk_ssim_workspace_size": (C.c_size_t, [C.c_int32] * 4),
     "vsrk_ssim": (C.c_int, [_P, _P] + [C.c_int32] * 5 + [C.c_float] * 3 + [_P, _P, _P, C.c_size_t, _P]),
     "vsrk_ssim3d_workspace_size": (C.c_size_t, [C.c_int32] * 5),

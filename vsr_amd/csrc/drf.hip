@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void prelu_partial_kernel(View y, View dx, int
 // loop over the 2048 partials was a chain of 8 dependent loads per lane)
 __global__ __launch_bounds__(1024) void prelu_final_kernel(const double* __restrict__ part, int nblk,
                                                            const float* __restrict__ a, float* __restrict__ da,
-                                                           int accumulate) {
+                                                           int accumulate, int pre = 0) {
   __shared__ double sh[1024];
   double s = 0.0;
   for (int b = threadIdx.x; b < nblk; b += 2048) {
@@ -155,7 +155,8 @@ __global__ __launch_bounds__(1024) void prelu_final_kernel(const double* __restr
     // A slope <= 0 makes the output-based gradient ambiguous, so it poisons
     // da with NaN (a loud failure in the optimizer step, never a silently
     // wrong gradient); nn.PReLU starts at 0.2 (drf_net.py:56).
-    const float v = av > 0.0 ? (float)(sh[0] / (av * av)) : __builtin_nanf("");
+    // (pre: the partials are already sum_{x<0} g x, any slope)
+    const float v = pre ? (float)sh[0] : av > 0.0 ? (float)(sh[0] / (av * av)) : __builtin_nanf("");
     *da = accumulate ? *da + v : v;
   }
 }
@@ -229,8 +230,13 @@ namespace {
 // div/mod chain and moved single bf16 elements: 99 us per call, 21 % of the
 // DRF step.
 template <typename T>
+// pre = 0: y is the PReLU OUTPUT (x < 0 read as y < 0, exact while a > 0):
+// slope partials sum dx * y, divided by a^2 in prelu_final_kernel.
+// pre = 1: y is the PRE-ACTIVATION x (nn.PReLU's own saved input, any a):
+// dx = x > 0 ? g : a g, slope partials sum_{x<0} g x (g = dy [+ dy2] in fp32)
 __global__ __launch_bounds__(256) void prelu_bwd_kernel(View y, View dy, View dy2, int has2, const float* __restrict__ a,
-                                                        View dx, int nrows, int vec, double* __restrict__ part) {
+                                                        View dx, int nrows, int vec, double* __restrict__ part,
+                                                        int pre) {
   constexpr int E = 16 / sizeof(T);
   const int C = y.c;
   const int cpv = (C + E - 1) / E;
@@ -289,7 +295,7 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(View y, View dy, View dy
             float acc = 0.f;
 #pragma unroll
             for (int e = 0; e < E; ++e)
-              if (yv[e] < 0.f) acc = fmaf(orr[e], yv[e], acc);
+              if (yv[e] < 0.f) acc = fmaf(pre ? g[e] : orr[e], yv[e], acc);
             s += acc;
           }
         }
@@ -319,7 +325,7 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(View y, View dy, View dy
           Chunk<T>::unpack(ov, orr);  // the rounded stored value, as in the reference's dtype
 #pragma unroll
           for (int e = 0; e < E; ++e)
-            if (yv[e] < 0.f) acc = fmaf(orr[e], yv[e], acc);
+            if (yv[e] < 0.f) acc = fmaf(pre ? g[e] : orr[e], yv[e], acc);
         } else {
 #pragma unroll
           for (int e = 0; e < E; ++e) {
@@ -329,7 +335,7 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(View y, View dy, View dy
               if (has2) g += to_f32<T>(pg2[e]);
               const T o = from_f32<T>(yv > 0.f ? g : av * g);
               po[e] = o;
-              if (yv < 0.f) acc = fmaf(to_f32<T>(o), yv, acc);
+              if (yv < 0.f) acc = fmaf(pre ? g : to_f32<T>(o), yv, acc);
             }
           }
         }
@@ -348,9 +354,9 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(View y, View dy, View dy
 }
 }  // namespace
 
-extern "C" int vsrk_prelu_bwd(const vsrk_tensor5* y, const vsrk_tensor5* dy, const vsrk_tensor5* dy2, const float* a,
-                              const vsrk_tensor5* dx, float* da, int32_t accumulate_da, void* workspace,
-                              size_t workspace_bytes, void* stream) {
+static int prelu_bwd_impl(const vsrk_tensor5* y, const vsrk_tensor5* dy, const vsrk_tensor5* dy2, const float* a,
+                          const vsrk_tensor5* dx, float* da, int32_t accumulate_da, void* workspace,
+                          size_t workspace_bytes, void* stream, int pre) {
   VSRK_CHECK(y && dy && dx && a && da && y->ptr && dy->ptr && dx->ptr, "prelu_bwd: null argument");
   for (const vsrk_tensor5* t : {dy, dy2, dx}) {
     if (!t) continue;
@@ -374,13 +380,25 @@ extern "C" int vsrk_prelu_bwd(const vsrk_tensor5* y, const vsrk_tensor5* dy, con
   hipStream_t s = (hipStream_t)stream;
   double* part = (double*)workspace;
   if (y->dtype == VSRK_BF16)
-    prelu_bwd_kernel<bf16><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, (int)nr64, vec, part);
+    prelu_bwd_kernel<bf16><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, (int)nr64, vec, part, pre);
   else if (y->dtype == VSRK_F16)
-    prelu_bwd_kernel<f16><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, (int)nr64, vec, part);
+    prelu_bwd_kernel<f16><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, (int)nr64, vec, part, pre);
   else
-    prelu_bwd_kernel<float><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, (int)nr64, vec, part);
+    prelu_bwd_kernel<float><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, (int)nr64, vec, part, pre);
   VSRK_LAUNCH_CHECK("prelu_bwd");
-  prelu_final_kernel<<<1, 1024, 0, s>>>(part, PRELU_BLOCKS, a, da, accumulate_da);
+  prelu_final_kernel<<<1, 1024, 0, s>>>(part, PRELU_BLOCKS, a, da, accumulate_da, pre);
   VSRK_LAUNCH_CHECK("prelu_final");
   return VSRK_OK;
+}
+
+extern "C" int vsrk_prelu_bwd(const vsrk_tensor5* y, const vsrk_tensor5* dy, const vsrk_tensor5* dy2, const float* a,
+                              const vsrk_tensor5* dx, float* da, int32_t accumulate_da, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  return prelu_bwd_impl(y, dy, dy2, a, dx, da, accumulate_da, workspace, workspace_bytes, stream, 0);
+}
+
+extern "C" int vsrk_prelu_bwd_pre(const vsrk_tensor5* x, const vsrk_tensor5* dy, const vsrk_tensor5* dy2,
+                                  const float* a, const vsrk_tensor5* dx, float* da, int32_t accumulate_da,
+                                  void* workspace, size_t workspace_bytes, void* stream) {
+  return prelu_bwd_impl(x, dy, dy2, a, dx, da, accumulate_da, workspace, workspace_bytes, stream, 1);
 }

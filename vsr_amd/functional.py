@@ -676,16 +676,20 @@ def prelu_wgrad(y: torch.Tensor, dx: torch.Tensor, a: torch.Tensor, da: torch.Te
 
 
 def prelu_bwd(y: torch.Tensor, dy: torch.Tensor, a: torch.Tensor, dx: torch.Tensor, da: torch.Tensor,
-              accumulate_da: bool, dy2: torch.Tensor | None = None) -> torch.Tensor:
-    """dx = (dy [+ dy2]) * (y > 0 ? 1 : a); da [+]= sum_{y<0} dx*y/a^2 (one pass)."""
+              accumulate_da: bool, dy2: torch.Tensor | None = None, pre: bool = False) -> torch.Tensor:
+    """dx = (dy [+ dy2]) * (y > 0 ? 1 : a); da [+]= sum_{y<0} dx*y/a^2 (one
+    pass) for the PReLU output y (exact while a > 0).  pre=True: y is the
+    pre-activation x (vsrk_prelu_bwd_pre, any slope): dx = g (x > 0 ? 1 : a),
+    da [+]= sum_{x<0} g x with g = dy [+ dy2]."""
     lib = _lib()
     nb = lib.vsrk_prelu_workspace_size()
     ws = workspace(nb, y.device)
     yv, gv, ov = N.t5(y), N.t5(dy), N.t5(dx)
     g2 = N.t5(dy2) if dy2 is not None else None
-    N.check(lib.vsrk_prelu_bwd(C.byref(yv), C.byref(gv), C.byref(g2) if g2 is not None else None, a.data_ptr(),
-                               C.byref(ov), da.data_ptr(), 1 if accumulate_da else 0, ws.data_ptr(), ws.numel(),
-                               N.stream_ptr(y.device)), "prelu_bwd")
+    fn = lib.vsrk_prelu_bwd_pre if pre else lib.vsrk_prelu_bwd
+    N.check(fn(C.byref(yv), C.byref(gv), C.byref(g2) if g2 is not None else None, a.data_ptr(),
+               C.byref(ov), da.data_ptr(), 1 if accumulate_da else 0, ws.data_ptr(), ws.numel(),
+               N.stream_ptr(y.device)), "prelu_bwd_pre" if pre else "prelu_bwd")
     return dx
 
 

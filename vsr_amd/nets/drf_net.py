@@ -196,6 +196,27 @@ class _DRFBase(BaseNet):
 
         return pw, sp
 
+    def _slopes_async(self):
+        """The PReLU slopes, copied to the host without a sync: the backward
+        reads them (the copy long done by then) to choose, per PReLU, the
+        output-based backward (exact while a > 0) or the pre-activation one
+        (nn.PReLU's own, any slope; the pre-activation is recomputed from the
+        tape).  Inside graph capture nothing is copied and every PReLU takes
+        the output-based form, whose slope gradient is NaN for a <= 0 (loud)."""
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        prelus = [m for m in self.modules() if isinstance(m, nn.PReLU)]
+        sl = torch.cat([m.weight.detach().reshape(-1) for m in prelus])
+        host = torch.empty(sl.shape, dtype=sl.dtype, pin_memory=True)
+        host.copy_(sl, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        idx, i = {}, 0
+        for m in prelus:
+            idx[id(m)] = (i, m.weight.numel())
+            i += m.weight.numel()
+        return host, ev, idx
+
     def _ups(self):
         steps = _up_steps(self.upscale_factor)
         return [(getattr(self.out_block, f"conv{j}"), s) for j, s in enumerate(steps, start=1)]
@@ -297,7 +318,7 @@ class _DRFBase(BaseNet):
                                  tail_in=u))
             X0 = X0n
         if tape is not None:
-            tape.update(recs=recs, shape=(b, h, w), packer=(pw, sp))
+            tape.update(recs=recs, shape=(b, h, w), packer=(pw, sp), slopes=self._slopes_async())
         return outs
 
     def _backward(self, tape: dict, gys) -> dict:
@@ -308,6 +329,11 @@ class _DRFBase(BaseNet):
         H, W = h * s, w * s
         pw, sp = tape["packer"]
         ib, fb = self.in_block, self.f_block
+        nonpos = set()  # PReLUs with a slope <= 0: the pre-activation backward
+        if tape.get("slopes") is not None:
+            host, ev, idx = tape["slopes"]
+            ev.synchronize()
+            nonpos = {k for k, (i, n) in idx.items() if bool((host[i:i + n] <= 0).any())}
         recs = tape["recs"]
         dev = recs[0]["X0"].device
         if not isinstance(gys, (tuple, list)):
@@ -436,8 +462,13 @@ class _DRFBase(BaseNet):
 
             defer(conv.weight, t, x, dy, run, acc)
 
-        def prelu(y, dy, pr, out, dy2=None):
+        def prelu(y, dy, pr, out, dy2=None, pre=None):
+            """PReLU backward from its output y; for a slope <= 0 from the
+            pre-activation that pre() recomputes from the tape (the producing
+            conv without its activation), as nn.PReLU does (drf_net.py:55-58)"""
             da, acc = gbuf(pr.weight)
+            if id(pr) in nonpos:
+                return F.prelu_bwd(pre(), dy, pr.weight, out, da, acc, dy2=dy2, pre=True)
             return F.prelu_bwd(y, dy, pr.weight, out, da, acc, dy2=dy2)
 
         co = self.out_channels
@@ -463,7 +494,9 @@ class _DRFBase(BaseNet):
             gfeat = du  # grad of features = in_features + f_features
             L, Hc, X0 = rc["L"], rc["Hc"], rc["X0"]
             # f_block out: f_features feeds the skip and the next frame's hidden state
-            gout = prelu(rc["ffeat"], gfeat, fb.out_block.prelu, sbuf("gout", t, h, w, f), dy2=d_hidden)
+            gout = prelu(rc["ffeat"], gfeat, fb.out_block.prelu, sbuf("gout", t, h, w, f), dy2=d_hidden,
+                         pre=lambda: F.conv(L[..., f:], pw(fb.out_block.conv), new(h, w, f), K1, P0,
+                                            bias=fb.out_block.conv.bias))
             wgrad(fb.out_block.conv, L[..., f:], gout, K1, P0, t)
             # Concat gradients without zero fills (the high-res one is 0.5 GB
             # per frame at cfg 3): the first contributor to a slice writes it,
@@ -480,8 +513,11 @@ class _DRFBase(BaseNet):
                 # down projection -> lr_{i+1} = L[..., (i+1)f:(i+2)f]
                 cv, cpr = (dn.conv, dn.prelu) if i == 0 else (dn.conv2, dn.prelu2)
                 sl = slice((i + 1) * f, (i + 2) * f)
-                gl = prelu(L[..., sl], dL[..., sl], cpr, sbuf(f"gl{i}", t, h, w, f))
                 hsrc = Hc[..., :f] if i == 0 else rc["t2s"][i]
+                gl = prelu(L[..., sl], dL[..., sl], cpr, sbuf(f"gl{i}", t, h, w, f),
+                           pre=lambda cv=cv, hsrc=hsrc: F.conv(
+                               hsrc, sp(cv, False)[0], new(h, w, f), K3, P1, bias=sp(cv, False)[1], x_shuffle=s,
+                               subpixel=F.subpixel_code(k, s, p, False, False)))
                 sp_wgrad(cv, hsrc, gl, False, t)
                 wq1, _ = sp(cv, False, 1)
                 spc = F.subpixel_code(k, s, p, False, True)
@@ -490,8 +526,12 @@ class _DRFBase(BaseNet):
                 else:
                     dt2 = sbuf(f"dt2_{i}", t, H, W, f)
                     da, acc = gbuf(dn.prelu1.weight)
-                    if not F.conv_prelu_bwd(gl, wq1, dt2, K3, P1, rc["t2s"][i], dn.prelu1.weight, da, acc,
-                                            y_shuffle=s, subpixel=spc):
+                    if id(dn.prelu1) in nonpos:  # slope <= 0: from the recomputed pre-activation
+                        F.conv(gl, wq1, dt2, K3, P1, y_shuffle=s, subpixel=spc)
+                        x2 = F.conv(Hc[..., :(i + 1) * f], pw(dn.conv1), new(H, W, f), K1, P0, bias=dn.conv1.bias)
+                        F.prelu_bwd(x2, dt2, dn.prelu1.weight, dt2, da, acc, pre=True)
+                    elif not F.conv_prelu_bwd(gl, wq1, dt2, K3, P1, rc["t2s"][i], dn.prelu1.weight, da, acc,
+                                              y_shuffle=s, subpixel=spc):
                         F.conv(gl, wq1, dt2, K3, P1, y_shuffle=s, subpixel=spc)
                         F.prelu_bwd(rc["t2s"][i], dt2, dn.prelu1.weight, dt2, da, acc)
                     wgrad(dn.conv1, Hc[..., :(i + 1) * f], dt2, K1, P0, t)
@@ -499,8 +539,11 @@ class _DRFBase(BaseNet):
                 # up projection -> hr_i = Hc[..., i f:(i+1) f]
                 dec, dpr = (up.deconv, up.prelu) if i == 0 else (up.deconv2, up.prelu2)
                 sh = slice(i * f, (i + 1) * f)
-                gh = prelu(Hc[..., sh], dHc[..., sh], dpr, sbuf(f"gh{i}", t, H, W, f))
                 src = L[..., :f] if i == 0 else rc["t1s"][i]
+                gh = prelu(Hc[..., sh], dHc[..., sh], dpr, sbuf(f"gh{i}", t, H, W, f),
+                           pre=lambda dec=dec, src=src: F.conv(
+                               src, sp(dec, True)[0], new(H, W, f), K3, P1, bias=sp(dec, True)[1], bias_r=1,
+                               y_shuffle=s, subpixel=F.subpixel_code(k, s, p, True, False)))
                 sp_wgrad(dec, src, gh, True, t)
                 wq1, _ = sp(dec, True, 1)
                 spc = F.subpixel_code(k, s, p, True, True)
@@ -509,13 +552,18 @@ class _DRFBase(BaseNet):
                 else:
                     dt1 = sbuf(f"dt1_{i}", t, h, w, f)
                     da, acc = gbuf(up.prelu1.weight)
-                    if not F.conv_prelu_bwd(gh, wq1, dt1, K3, P1, rc["t1s"][i], up.prelu1.weight, da, acc,
-                                            x_shuffle=s, subpixel=spc):
+                    if id(up.prelu1) in nonpos:  # slope <= 0: from the recomputed pre-activation
+                        F.conv(gh, wq1, dt1, K3, P1, x_shuffle=s, subpixel=spc)
+                        x1 = F.conv(L[..., :(i + 1) * f], pw(up.conv1), new(h, w, f), K1, P0, bias=up.conv1.bias)
+                        F.prelu_bwd(x1, dt1, up.prelu1.weight, dt1, da, acc, pre=True)
+                    elif not F.conv_prelu_bwd(gh, wq1, dt1, K3, P1, rc["t1s"][i], up.prelu1.weight, da, acc,
+                                              x_shuffle=s, subpixel=spc):
                         F.conv(gh, wq1, dt1, K3, P1, x_shuffle=s, subpixel=spc)
                         F.prelu_bwd(rc["t1s"][i], dt1, up.prelu1.weight, dt1, da, acc)
                     wgrad(up.conv1, L[..., :(i + 1) * f], dt1, K1, P0, t)
                     F.conv(dt1, pw(up.conv1, 1), dL[..., :(i + 1) * f], K1, P0, accumulate=True)
-            g0 = prelu(L[..., :f], dL[..., :f], fb.in_block.prelu, sbuf("g0", t, h, w, f))
+            g0 = prelu(L[..., :f], dL[..., :f], fb.in_block.prelu, sbuf("g0", t, h, w, f),
+                       pre=lambda: F.conv(X0, pw(fb.in_block.conv), new(h, w, f), K1, P0, bias=fb.in_block.conv.bias))
             wgrad(fb.in_block.conv, X0, g0, K1, P0, t)
             dX0 = F.conv(g0, pw(fb.in_block.conv, 1), new(h, w, 2 * f), K1, P0)
             if t == 0:  # the first hidden state is in_features itself
@@ -523,10 +571,12 @@ class _DRFBase(BaseNet):
                 d_hidden = None
             else:
                 d_hidden = dX0[..., f:]
-            gin = prelu(X0[..., :f], gfeat, ib.prelu2, sbuf("gin", t, h, w, f), dy2=dX0[..., :f])
+            gin = prelu(X0[..., :f], gfeat, ib.prelu2, sbuf("gin", t, h, w, f), dy2=dX0[..., :f],
+                        pre=lambda: F.conv(rc["u1"], pw(ib.conv2), new(h, w, f), K1, P0, bias=ib.conv2.bias))
             wgrad(ib.conv2, rc["u1"], gin, K1, P0, t)
             du1 = F.conv(gin, pw(ib.conv2, 1), sbuf("du_u1", t, h, w, 4 * f), K1, P0)
-            prelu(rc["u1"], du1, ib.prelu1, du1)
+            prelu(rc["u1"], du1, ib.prelu1, du1,
+                  pre=lambda: F.conv(rc["xv"], pw(ib.conv1), new(h, w, 4 * f), K3, P1, bias=ib.conv1.bias))
             wgrad(ib.conv1, rc["xv"], du1, K3, P1, t)
             launch_runs(t)
         for prm, g in bufs.values():
