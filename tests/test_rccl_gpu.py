@@ -1,0 +1,82 @@
+"""The RCCL (torch.distributed "nccl") path on one GPU (VERDICT r4 item 11 /
+ADVICE r4: the 8-GPU runs are the driver's; the test box has one GPU, so the
+RCCL branches -- device tensors in the bucketed gradient all-reduce, the
+device-side SyncBN global count and the async backward all-reduces whose
+wait() only orders the stream -- run here as a world of one rank, with the
+SyncBN hook forced on).  One rank's all-reduce is the identity, so the step
+must equal the same step without any process group: outputs, gradients and
+running statistics within fp32 / bf16 summation noise, every gradient bucket a
+view of the all-reduced storage."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _step(precision, ddp, q=None, port=None):
+    import torch.nn.functional as Fn
+    from vsr_amd import nets
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    if ddp:
+        import torch.distributed as dist
+        from vsr_amd.ddp import GradSync, SyncBNAllReduce
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        torch.manual_seed(5)
+        net = nets.DUFNet(1, 1, 7, 5, 4, "_DenseLayer16").to(dev).set_precision(precision).train()
+        g = torch.Generator().manual_seed(6)
+        x = [torch.randn((4, 1, 10, 12), generator=g).to(dev) for _ in range(7)]
+        y = torch.randn((4, 1, 40, 48), generator=g).to(dev)
+        sync = None
+        if ddp:
+            assert dist.get_backend() == "nccl"
+            sync = GradSync(net, 1)
+            net.bn_allreduce = SyncBNAllReduce(None)  # forced: enable_sync_bn skips a world of one
+        out = net(x)
+        Fn.l1_loss(out, y).backward()
+        if sync is not None:
+            sync.finish()
+        torch.cuda.synchronize()
+        res = {"out": out.detach().cpu().numpy(),
+               "grads": {k: p.grad.detach().cpu().numpy() for k, p in net.named_parameters()},
+               "buffers": {k: v.detach().cpu().numpy() for k, v in net.state_dict().items() if "running" in k}}
+        if q is None:
+            return res
+        q.put(res)
+    finally:
+        if ddp:
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_rccl_one_rank_equals_no_group(precision):
+    ref = _step(precision, False)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_step, args=(precision, True, q, _port()))
+    p.start()
+    got = q.get(timeout=240)
+    p.join(60)
+    assert p.exitcode == 0
+    tol = 1e-5 if precision == "fp32" else 1e-2
+    assert abs(got["out"] - ref["out"]).max() <= tol * (1 + abs(ref["out"]).max())
+    gmax = max(float((v ** 2).sum()) ** 0.5 for v in ref["grads"].values())
+    for k, v in ref["grads"].items():
+        d = float(((got["grads"][k] - v) ** 2).sum()) ** 0.5
+        assert d <= tol * max(float((v ** 2).sum()) ** 0.5, 1e-3 * gmax), (k, d)
+    for k, v in ref["buffers"].items():
+        assert abs(got["buffers"][k] - v).max() <= tol * (1 + abs(v).max()), k
