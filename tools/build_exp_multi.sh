@@ -12,7 +12,8 @@ pids=""
 for S in $SRCS; do
   STEM=$(basename $S .hip)
   OBJS=$(echo "$OBJS" | grep -v "/$STEM.o$")
-  /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wno-unused-result -I include "$@" -c vsr_amd/csrc/$S -o $D/$STEM.o &
+  XF=$(python -c "import sys; sys.path.insert(0, '.'); from vsr_amd.build import SRC_FLAGS; print(' '.join(SRC_FLAGS.get('$S', [])))")
+  /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wno-unused-result $XF -I include "$@" -c vsr_amd/csrc/$S -o $D/$STEM.o &
   pids="$pids $!"
 done
 for p in $pids; do wait $p; done

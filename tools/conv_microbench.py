@@ -120,10 +120,13 @@ def main():
               f"({flop / ms / 1e9 / 2500 * 100:.1f}% of 2.5 PF)  "
               f"{nbytes.get(name, 0) / ms / 1e9:7.2f} TB/s (min HBM bytes)", flush=True)
         if args.stamps:
-            stamp_report(fn)
+            if name.startswith("wgrad"):
+                stamp_report(fn, "vsrk_wroll_stamps", ["wait", "barrier", "compute"])
+            else:
+                stamp_report(fn)
 
 
-def stamp_report(fn):
+def stamp_report(fn, sym="vsrk_roll_stamps", names=("wait", "barrier", "flush", "compute")):
     """Per-step cycle split of waves 0 and 4 (one SIMD) of workgroups 0-15
     from a conv_roll.hip ROLL_STAMP build: stage wait, barrier, flush
     (epilogue), compute."""
@@ -133,11 +136,11 @@ def stamp_report(fn):
     fn()
     torch.cuda.synchronize()
     buf = (ctypes.c_uint * (16 * 2 * 128))()
-    if lib.vsrk_roll_stamps(buf) != 0:
-        raise RuntimeError("vsrk_roll_stamps failed")
+    if getattr(lib, sym)(buf) != 0:
+        raise RuntimeError(f"{sym} failed")
     st = np.frombuffer(buf, dtype=np.uint32).reshape(32, 128).astype(np.int64)
-    names = ["wait", "barrier", "flush", "compute"]
-    tot = np.zeros(4)
+    ne = len(names)
+    tot = np.zeros(ne)
     cnt = 0
     for w in range(32):
         s = st[w]
@@ -145,16 +148,16 @@ def stamp_report(fn):
             continue
         d = np.diff(s) % (1 << 32)
         # d[i] = stamp[i+1] - stamp[i]: event (i+1) % 4 ends the phase
-        per = np.zeros(4)
+        per = np.zeros(ne)
         for i, v in enumerate(d):
-            per[(i + 1) % 4] += v
+            per[(i + 1) % ne] += v
         tot += per
         cnt += 1
         if w in (0, 1):
             print(f"  wg{w // 2} wave{4 * (w % 2)}: " + " ".join(
-                f"{names[(i + 1) % 4][0]}{int(v)}" for i, v in enumerate(d[:40])))
+                f"{names[(i + 1) % ne][0]}{int(v)}" for i, v in enumerate(d[:40])))
     if cnt:
-        steps = 127 / 4
+        steps = 127 / ne
         print("  mean cycles per step: " + "  ".join(f"{n} {tot[i] / cnt / steps:8.0f}" for i, n in enumerate(names)))
 
 

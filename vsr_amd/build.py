@@ -18,6 +18,12 @@ INCLUDE = ROOT.parent / "include"
 ARCH = os.environ.get("VSRK_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+# Per-source extra flags.  The rolling convs: no SLP vectorisation -- it
+# packed the BN prologue / epilogue into v_pk_fma_f32 with a v_mov per
+# operand pair to marshal the packed registers (76 -> 28 v_mov per weight-
+# gradient stage), and packed f32 VALU beside MFMAs costs more issue than the
+# scalar form (MI355X_MICROARCH.md, cycle constants).
+SRC_FLAGS = {"conv_roll.hip": ["-fno-slp-vectorize"], "conv_wgrad_roll.hip": ["-fno-slp-vectorize"]}
 
 
 def sources() -> list[Path]:
@@ -30,6 +36,7 @@ def _digest() -> str:
         h.update(p.name.encode())
         h.update(p.read_bytes())
     h.update(" ".join(FLAGS).encode())
+    h.update(repr(sorted(SRC_FLAGS.items())).encode())
     return h.hexdigest()[:16]
 
 
@@ -72,11 +79,12 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         # per-object stamp: recompile only when this source, a header it
         # includes (transitively) or the flags changed
         deps = b"".join(p.read_bytes() for p in _includes(src))
-        key = hashlib.sha256(src.read_bytes() + deps + " ".join(FLAGS).encode()).hexdigest()[:16]
+        flags = FLAGS + SRC_FLAGS.get(src.name, [])
+        key = hashlib.sha256(src.read_bytes() + deps + " ".join(flags).encode()).hexdigest()[:16]
         ostamp = objdir / (src.stem + ".stamp")
         if not force and obj.exists() and ostamp.exists() and ostamp.read_text() == key:
             return obj
-        cmd = [HIPCC, *FLAGS, "-I", str(INCLUDE), "-c", str(src), "-o", str(obj)]
+        cmd = [HIPCC, *flags, "-I", str(INCLUDE), "-c", str(src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

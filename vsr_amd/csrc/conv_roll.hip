@@ -394,7 +394,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     d.use = (k.m & qa) | ((km & 1) ? qkd0 : 0u) | ((km & 2) ? qkd1 : 0u) | ((km & 4) ? qkd2 : 0u);
     return d;
   };
-  auto dma = [&](const Dma& d, int q, int slot) __attribute__((always_inline)) {
+  auto dma = [&](Dma d, int q, int slot) __attribute__((always_inline)) {
     const int j = wave + RNW * q;
     const H* base = ((qa >> q) & 1) ? d.xb : d.wsrc;
     const void* src = ((d.use >> q) & 1) ? (const void*)(base + rel[q]) : (const void*)zp;
@@ -501,7 +501,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // ahead (slot SLOT+2); the remaining groups apply the BN/ReLU prologue to
   // this wave's A pieces of the NEXT stage (slot SLOT+1, landed one stage
   // ago), beside the MFMAs instead of in front of the barrier.
-  auto compute = [&](auto slot_c, int P, unsigned km, const Dma& dn, bool don, bool tnext, int tc,
+  auto compute = [&](auto slot_c, int P, unsigned km, Dma dn, bool don, bool tnext, int tc,
                      unsigned tm, unsigned tk0, unsigned tk1, int cchunk) __attribute__((always_inline)) {
     constexpr int SLOT = decltype(slot_c)::value;
     const char* sl = lds + SLOT * RSLOT;

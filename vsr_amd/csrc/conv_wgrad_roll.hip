@@ -78,6 +78,16 @@ struct WRArgs {
 };
 
 __device__ __attribute__((aligned(256))) uint4 g_wroll_zero[16];
+#ifdef ROLL_STAMP
+// Diagnostic builds only (tools/conv_microbench.py --stamps): s_memtime
+// stamps of waves 0 and 4 (one SIMD) of workgroups 0-15 kept in VGPR lanes,
+// stored at exit: per step [after the stage wait, after the barrier, after
+// compute]
+#ifndef ROLL_STAMP_SKIP
+#define ROLL_STAMP_SKIP 8
+#endif
+__device__ unsigned g_wroll_stamp[16 * 2 * 128];
+#endif
 
 #ifndef WR_XWIN
 #define WR_XWIN 1
@@ -250,7 +260,7 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
     d.use = w.m & ((xok ? qx : 0u) | (yok ? qy : 0u));
     return d;
   };
-  auto dma = [&](const Dma& d, int q, int xs, int ys) __attribute__((always_inline)) {
+  auto dma = [&](Dma d, int q, int xs, int ys) __attribute__((always_inline)) {
     const int j = wave + WNW * q;
     const H* base = ((qx >> q) & 1) ? d.xb : d.yb;
     const void* src = ((d.use >> q) & 1) ? (const void*)(base + rel[q]) : (const void*)zp;
@@ -285,7 +295,7 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
   // per kd), then per kh the 3 kw fragments of x row r + kh and 3 x 3 MFMAs
   // (kd active x kw).  DMA pieces of the stage two ahead: 2 per row; the late
   // prologue of the next stage: in the last row.
-  auto compute = [&](auto xs_c, const uint32_t* yoff, unsigned km, bool newy, const Dma& dn, bool don, int xs2,
+  auto compute = [&](auto xs_c, const uint32_t* yoff, unsigned km, bool newy, Dma dn, bool don, int xs2,
                      int ys2, bool tnext, unsigned tm) __attribute__((always_inline)) {
     constexpr int XS = decltype(xs_c)::value;
     const char* xsl = lds + XS * WXSLOT;
@@ -334,14 +344,27 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
           for (int q = 2 * (r - 2); q < 2 * (r - 1); ++q) transform_piece((XS + 1) % 3, q, tm);
         }
       }
+#if WR_XWIN
+      // kd outermost: one branch per (row, kd) for the inactive taps of a
+      // slice near the tile's depth ends (12 per stage; per (row, kh, kd)
+      // there were 36, each a scalar test and branch between MFMA groups)
+#pragma unroll
+      for (int kd = 0; kd < 3; ++kd) {
+        if ((km >> kd) & 1) {
+#pragma unroll
+          for (int kh = 0; kh < 3; ++kh) {
+            const uint4* xf = xw[(r + kh) % 3];
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw)
+              acc[kd][kh][kw] = mfma16(__builtin_bit_cast(V8, yf[kd]), __builtin_bit_cast(V8, xf[kw]), acc[kd][kh][kw]);
+          }
+        }
+      }
+#else
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
-#if WR_XWIN
-        const uint4* xf = xw[(r + kh) % 3];
-#else
         uint4 xf[3];
         load_x(xf, r + kh);
-#endif
 #pragma unroll
         for (int kd = 0; kd < 3; ++kd) {
           if ((km >> kd) & 1) {
@@ -351,6 +374,7 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
           }
         }
       }
+#endif
       if (do_bias && cih == 0 && newy)
         bacc = mfma16(__builtin_bit_cast(V8, yf[0]), __builtin_bit_cast(V8, ones), bacc);
     }
@@ -396,11 +420,27 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
       for (int q = 0; q < 4; ++q) transform_piece(0, q, cur.m);
     }
   }
+#ifdef ROLL_STAMP
+  unsigned stv0 = 0, stv1 = 0;
+  int stc = -3 * ROLL_STAMP_SKIP;
+  auto stamp = [&]() __attribute__((always_inline)) {
+    if (stc >= 0 && stc < 128) {
+      const unsigned tv = (unsigned)__builtin_amdgcn_s_memtime();
+      if (stc < 64) stv0 = lane == stc ? tv : stv0;
+      else stv1 = lane == stc - 64 ? tv : stv1;
+    }
+    ++stc;
+  };
+#else
+  auto stamp = [&]() __attribute__((always_inline)) {};
+#endif
   auto step = [&](auto xs_c) __attribute__((always_inline)) -> bool {
     constexpr int XS = decltype(xs_c)::value;
     if (tnext) wr_wait_vmcnt<WNQ>();
     else wr_wait_vmcnt<0>();
+    stamp();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    stamp();
     const int di = cur.tl.di_s + cur.k, P = di + a.pd;
     unsigned km = 0;
     if (di >= 0) {
@@ -417,6 +457,7 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
     dn.use = 0;
     if (vn) dn = prep(nx);
     compute(xs_c, yoff, km, newy, dn, vn, (XS + 2) % 3, (stage + 2) % 5, tnext, tm);
+    stamp();
     // the stage just issued (nx) is the next one's successor
     tnext = vn;
     tm = nx.m;
@@ -430,6 +471,13 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
     }
   }
 
+#ifdef ROLL_STAMP
+  if (blockIdx.x < 16 && (wave == 0 || wave == 4)) {
+    unsigned* o = g_wroll_stamp + (blockIdx.x * 2 + (wave >> 2)) * 128;
+    o[lane] = stv0;
+    o[64 + lane] = stv1;
+  }
+#endif
   // ---- slabs: split index 2 * split + row half, combo (kd, ci chunk, co tile) ----
   const int ncombo = 3 * a.nci_chunks * a.nco_tiles;
   const int l15 = lane & 15, lg = lane >> 4;
@@ -454,6 +502,14 @@ __global__ __launch_bounds__(WNW * 64, 2) void wgrad_roll_kernel(WRArgs a) {
     }
   }
 }
+
+#ifdef ROLL_STAMP
+}  // namespace
+extern "C" int vsrk_wroll_stamps(unsigned* dst) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_wroll_stamp), sizeof(g_wroll_stamp)) == hipSuccess ? 0 : 1;
+}
+namespace {
+#endif
 
 int g_wroll_mode = -1;  // -1: VSRK_WGRAD_ROLL (unset: 2), 0 off, 1 forced on, 2 automatic
 
