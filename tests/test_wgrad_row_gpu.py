@@ -112,3 +112,102 @@ def test_wgrad_row_edsr_layer_size():
     F.conv_wgrad(x, dy, (1, 3, 3), (0, 1, 1), dw0, db0)
     assert (dw - dw0).abs().max().item() <= 1e-4 * dw0.abs().max().item()
     assert (db - db0).abs().max().item() <= 1e-4 * db0.abs().max().item()
+
+
+# ---- sub-pixel views ----
+PROJ = {2: (6, 2, 2), 3: (7, 3, 2), 4: (8, 4, 2), 8: (12, 8, 2)}
+
+
+def _cl(t):  # (N,C,H,W) -> (N,1,H,W,C)
+    return t.permute(0, 2, 3, 1).unsqueeze(1).contiguous()
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("ci", [64, 128])
+def test_wgrad_row_edsr_upsampler(dt, ci):
+    """EDSR's Upsampler conv (edsr_net.py:15-30, nn.Conv2d(f, 4f, 3) then
+    PixelShuffle(2)): its output gradient is read straight from the high-res
+    gradient through a shuffle-2 view, the 4f logical channels permuted by
+    perm_r=2.  Equal to the pipelined kernel within fp32 summation noise, and
+    to the fp64 gradient of conv2d + pixel_shuffle."""
+    n, h, w, r = 2, 11, 37, 2
+    co = ci * r * r
+    g = torch.Generator().manual_seed(ci + 3)
+    x = torch.randn((n, 1, h, w, ci), generator=g).to(DEV, dt)
+    gy_hr = torch.randn((n, 1, h * r, w * r, ci), generator=g).to(DEV, dt)
+    dw = torch.empty((co, ci, 1, 3, 3), device=DEV)
+    db = torch.empty(co, device=DEV)
+    F.conv_wgrad(x, gy_hr, (1, 3, 3), (0, 1, 1), dw, db, perm_r=r, dy_shuffle=r)
+    # fp64: PixelShuffle's channel order c * r^2 + i * r + j
+    xn = x.double().cpu()[:, 0].permute(0, 3, 1, 2).requires_grad_(True)
+    wr = torch.zeros((co, ci, 3, 3), dtype=torch.float64, requires_grad=True)
+    br = torch.zeros(co, dtype=torch.float64, requires_grad=True)
+    yo = torch.nn.functional.pixel_shuffle(torch.nn.functional.conv2d(xn, wr, br, padding=1), r)
+    yo.backward(gy_hr.double().cpu()[:, 0].permute(0, 3, 1, 2))
+    rw = wr.grad.view(co, ci, 1, 3, 3)
+    tol = 1e-4 * rw.abs().max().item()
+    assert (dw.double().cpu() - rw).abs().max().item() <= tol
+    assert (db.double().cpu() - br.grad).abs().max().item() <= 1e-4 * br.grad.abs().max().item()
+    F.set_conv_path("wgrad_row", 0)
+    dw0, db0 = torch.empty_like(dw), torch.empty_like(db)
+    F.conv_wgrad(x, gy_hr, (1, 3, 3), (0, 1, 1), dw0, db0, perm_r=r, dy_shuffle=r)
+    assert (dw - dw0).abs().max().item() <= tol
+    assert (db - db0).abs().max().item() <= 1e-4 * db0.abs().max().item()
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("r", [2, 3, 4, 8])
+@pytest.mark.parametrize("skip", [False, True])
+def test_wgrad_row_drf_projections(dt, r, skip):
+    """DRF's feedback-block projections (drf_net.py:70-102) at f = 64: the
+    ConvTranspose2d(k, s, p) weight gradient with dy a shuffle-s view of the
+    high-res gradient, the strided Conv2d's with x a shuffle-s view of the
+    high-res input.  With the sub-pixel code passed (a form the router keeps on
+    the pipelined kernel unless forced), each phase's zero taps are skipped and
+    come out exactly zero, like the pipelined kernel's.  Folded to
+    the k x k weights against fp64 autograd; unfolded against the pipelined
+    kernel."""
+    k, s, p = PROJ[r]
+    f = 64
+    n, h, w = 2, 7, 23 if r < 8 else 9
+    H, W = h * s, w * s
+    g = torch.Generator().manual_seed(r * 7 + skip)
+    x_lr = torch.randn((n, f, h, w), generator=g)
+    x_hr = torch.randn((n, f, H, W), generator=g)
+    gy_hr = torch.randn((n, f, H, W), generator=g)
+    gy_lr = torch.randn((n, f, h, w), generator=g)
+    K3, P1 = (1, 3, 3), (0, 1, 1)
+    for tr in (True, False):
+        code = F.subpixel_code(k, s, p, tr, False) if skip else 0
+        wk = torch.zeros((f, f, k, k), dtype=torch.float64, requires_grad=True)
+        bk = torch.zeros(f, dtype=torch.float64, requires_grad=True)
+        if tr:
+            xin, gin = _cl(x_lr).to(DEV, dt), _cl(gy_hr).to(DEV, dt)
+            kw = dict(dy_shuffle=s)
+            torch.nn.functional.conv_transpose2d(xin.double().cpu()[:, 0].permute(0, 3, 1, 2), wk, bk, stride=s,
+                                                 padding=p).backward(gin.double().cpu()[:, 0].permute(0, 3, 1, 2))
+        else:
+            xin, gin = _cl(x_hr).to(DEV, dt), _cl(gy_lr).to(DEV, dt)
+            kw = dict(x_shuffle=s)
+            torch.nn.functional.conv2d(xin.double().cpu()[:, 0].permute(0, 3, 1, 2), wk, bk, stride=s,
+                                       padding=p).backward(gin.double().cpu()[:, 0].permute(0, 3, 1, 2))
+        weq, beq = F.subpixel_conv_weight(torch.zeros((f, f, k, k), device=DEV), torch.zeros(f, device=DEV),
+                                          k, s, p, transposed=tr)
+        res = []
+        for row in (2, 0):  # 2: the tap-skip forms are forced onto the row kernel
+            F.set_conv_path("wgrad_row", row)
+            dweq, dbeq = torch.empty_like(weq), torch.empty_like(beq)
+            F.conv_wgrad(xin, gin, K3, P1, dweq.view(*weq.shape[:2], 1, 3, 3), dbeq, subpixel=code, **kw)
+            res.append((dweq, dbeq))
+        F.set_conv_path("wgrad_row", 1)
+        (dweq, dbeq), (dweq0, dbeq0) = res
+        tol = 1e-4 * dweq0.abs().max().item()
+        if skip:  # the skipped taps: exact zeros on both paths
+            assert torch.equal(dweq == 0, dweq0 == 0), tr
+        assert (dweq - dweq0).abs().max().item() <= tol, tr
+        assert (dbeq - dbeq0).abs().max().item() <= 1e-4 * dbeq0.abs().max().item(), tr
+        dw = torch.empty((f, f, k, k), device=DEV)
+        db = torch.empty(f, device=DEV)
+        F.subpixel_wgrad_fold(dweq, dbeq, dw, db, k, s, p, transposed=tr)
+        assert (dw.double().cpu() - wk.grad).abs().max().item() <= 1e-4 * wk.grad.abs().max().item(), tr
+        assert (db.double().cpu() - bk.grad).abs().max().item() <= 1e-4 * bk.grad.abs().max().item(), tr

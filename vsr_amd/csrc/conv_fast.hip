@@ -38,8 +38,9 @@ extern "C" int vsrk_conv_set_algo(int32_t mode) {
 }
 
 extern "C" int vsrk_conv_set_path(const char* path, int32_t mode) {
-  VSRK_CHECK(path && mode >= -1 && mode <= 1, "conv_set_path: mode must be -1, 0 or 1");
+  VSRK_CHECK(path, "conv_set_path: null path");
   const std::string p(path);
+  VSRK_CHECK(mode >= -1 && mode <= (p == "wgrad_row" ? 2 : 1), "conv_set_path: mode must be -1, 0 or 1 (wgrad_row: 2)");
   if (p == "fast") g_fast_mode = mode;
   else if (p == "thin") vsrk_g_thin_mode = mode;
   else if (p == "wgrad_pipe") vsrk_g_wgrad_pipe_mode = mode;

@@ -537,10 +537,12 @@ bool vsrk_wgrad_roll_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const 
     g_wroll_mode = !e ? 2 : (e[0] == '0' ? 0 : 1);
   }
   if (g_wroll_mode == 0) return false;
-  // automatic mode: with <= 3 output depths the kd-tap reuse of the rolling
-  // walk does not pay for its ring (DUF units 4 / 5: 1619 vs 1764 us and
-  // 755 vs 1159 us for the pipelined kernel, r3p microbench)
-  if (g_wroll_mode == 2 && dy->d <= 3 && vsrk_g_roll_dz == 0) return false;
+  // automatic mode: with a single output depth the kd-tap reuse of the
+  // rolling walk does not pay for its ring (DUF's last unit, 3 -> 1: 812 vs
+  // 982 us for the pipelined kernel); at 3 output depths it does since the
+  // round-5 loop order (DUF unit 5 at F = 192, 5 -> 3: 1495 vs 1703 us; it
+  // lost, 1764 vs 1619, in round 3)
+  if (g_wroll_mode == 2 && dy->d <= 1 && vsrk_g_roll_dz == 0) return false;
   if (!vsrk_is16(x->dtype) || dy->dtype != x->dtype) return false;
   if (d->kd != 3 || d->kh != 3 || d->kw != 3 || d->pd < 0 || d->pd > 2 || d->ph < 0 || d->ph > 2 || d->pw < 0 ||
       d->pw > 2)

@@ -95,9 +95,24 @@ __device__ __forceinline__ uint4 rw_frag(uint32_t p0, uint32_t p1) {
   return __builtin_bit_cast(uint4, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
+constexpr int RW_MAXB = 16;  // 64-channel blocks of a sub-pixel view (1024 logical channels)
+
 struct RowArgs {
   const char* x;   // element (n, d, h, w, c) at x + 2 * (n*xsn + d*xsd + h*xsh + w*xsw + c)
   const char* dy;
+  // element offset of 64-channel block b inside its operand: b * 64 for a
+  // plain view; for a sub-pixel view (shuffle r: logical channel
+  // (i r + j) C' + c' of LR voxel (h, w) at physical (r h + i, r w + j, c'))
+  // the block's phase row / column and c' base (its h / w strides above are
+  // then r physical rows / columns) -- EDSR's up-sampler and DRF's sub-pixel
+  // projections (edsr_net.py:59-62, drf_net.py:81-100)
+  int xoff[RW_MAXB], yoff[RW_MAXB];
+  // sub-pixel forms (SPM): per block of the shuffled operand, the taps its
+  // phase meets (bit kh * 3 + kw); the others are structurally zero in the
+  // equivalent weight (drf_net.py:70-102 at k = 2s: 4 of 9) -- their MFMAs
+  // are skipped and their slab entries written as zeros
+  uint16_t tapm[RW_MAXB];
+  int tapm_x;  // the mask belongs to the input block (x shuffled) or the output block
   float* ws;
   int64_t xsn, xsd, xsh, xsw, ysn, ysd, ysh, ysw;
   int xd, H, W;
@@ -106,7 +121,7 @@ struct RowArgs {
   int prio;  // A/B knob (VSRK_WGRAD_ROW_PRIO=1): s_setprio 1 around each group's MFMAs
 };
 
-template <typename H>
+template <typename H, bool SPM>
 __global__ __launch_bounds__(RW_NW * 64, 1) void wgrad_row_kernel(RowArgs a) {
   using V8 = typename V8R<H>::type;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -127,8 +142,9 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void wgrad_row_kernel(RowArgs a) {
   const int h0 = band * a.band_h;
   const int nst = min(a.H, h0 + a.band_h) - h0;  // output rows (stages)
   const int w0 = seg * RW_SEG;
-  const char* xim = a.x + 2 * (nb * a.xsn + dd * a.xsd + cic * 64);
-  const char* yim = a.dy + 2 * (nb * a.ysn + dd * a.ysd + cot * 64);
+  const unsigned tapm = SPM ? (unsigned)a.tapm[a.tapm_x ? cic : cot] : 0x1ffu;  // workgroup-uniform
+  const char* xim = a.x + 2 * (nb * a.xsn + dd * a.xsd + a.xoff[cic]);
+  const char* yim = a.dy + 2 * (nb * a.ysn + dd * a.ysd + a.yoff[cot]);
 
   // ---- per-lane piece roles (1 KB = 8 voxels x 64 channels), the same kind
   // for every wave at each q: q = 0, 1: x piece wave + 8q; q = 2, 3: dy piece
@@ -284,12 +300,14 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void wgrad_row_kernel(RowArgs a) {
       if (a.prio) __builtin_amdgcn_s_setprio(1);
       const int kc = G / 3, kh = G % 3;
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw)
+      for (int kw = 0; kw < 3; ++kw) {
+        if (SPM && !((tapm >> (kh * 3 + kw)) & 1)) continue;  // workgroup-uniform
 #pragma unroll
         for (int b = 0; b < 2; ++b)
           if (RW_ABL & 2) acc[kh][kw][b][0] += __builtin_bit_cast(float, yf[kc & 1][b].x ^ xf[G & 1][kw].y);
           else acc[kh][kw][b] = rw_mfma(__builtin_bit_cast(V8, yf[kc & 1][b]), __builtin_bit_cast(V8, xf[G & 1][kw]),
                                    acc[kh][kw][b]);
+      }
       if (kh == 1 && kc == cib) {  // wave-uniform
 #pragma unroll
         for (int b = 0; b < 2; ++b)
@@ -319,7 +337,7 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void wgrad_row_kernel(RowArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int co = 32 * coh + 16 * b + 4 * lg + i, ci = 16 * cib + l15;
-        out[(t9 * RW_COW + co) * 64 + ci] = acc[t9 / 3][t9 % 3][b][i];
+        out[(t9 * RW_COW + co) * 64 + ci] = ((tapm >> t9) & 1) ? acc[t9 / 3][t9 % 3][b][i] : 0.f;
       }
   if (a.want_bias && cic == 0) {  // workgroup-uniform
     // bacc[b][i] = dbias partial (k-chunk cib) of channel 32 coh + 16 b + 4 lg + i
@@ -339,7 +357,7 @@ __global__ __launch_bounds__(RW_NW * 64, 1) void wgrad_row_kernel(RowArgs a) {
   }
 }
 
-int g_wrow_mode = -1;  // -1: VSRK_WGRAD_ROW (unset: on), 0 off, 1 on
+int g_wrow_mode = -1;  // -1: VSRK_WGRAD_ROW (unset: on), 0 off, 1 on, 2 on with the sub-pixel tap skip forms
 
 int wrow_num_cus() {
   static int n = 0;
@@ -363,13 +381,31 @@ bool vsrk_wgrad_row_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const v
   if (g_wrow_mode == 0) return false;
   if (!vsrk_is16(x->dtype) || dy->dtype != x->dtype) return false;
   if (d->kd != 1 || d->kh != 3 || d->kw != 3 || d->pd != 0 || d->ph != 1 || d->pw != 1) return false;
-  if (d->prologue != VSRK_PRO_NONE || d->subpixel) return false;
-  if (x->shuffle > 1 || dy->shuffle > 1 || x->c % 64 || dy->c % 64) return false;
+  // (sub-pixel views: one operand is a shuffle-r view of a high-res buffer;
+  // with d->subpixel set, the taps a phase never meets are skipped, see tapm)
+  if (d->prologue != VSRK_PRO_NONE) return false;
+  if (x->c % 64 || dy->c % 64 || (x->shuffle > 1 && dy->shuffle > 1)) return false;
+  // Views with the sub-pixel tap skip (DRF's projections) stay on the
+  // pipelined kernel unless forced (mode 2): with 4 of 9 taps per phase the
+  // row pipeline is load-bound and its 9-tap slabs double the reduce -- cfg3
+  // A/B, same box: projection weight gradients 25.3 ms/step here vs 22.0 on the
+  // pipelined kernel (profiles/r5_wgrad_row_subpixel_ab.txt).  Plain
+  // shuffled views (EDSR's up-sampler, all taps live) run here.
+  if (d->subpixel && (x->shuffle > 1 || dy->shuffle > 1) && g_wrow_mode != 2) return false;
+  if (x->c / 64 > RW_MAXB || dy->c / 64 > RW_MAXB) return false;
+  for (const vsrk_tensor5* t : {x, dy}) {  // a sub-pixel view: every 64-channel block inside one phase
+    if (t->shuffle <= 1) continue;
+    const int r = t->shuffle, cph = t->c / (r * r);
+    if (cph * r * r != t->c || cph % 64) return false;
+  }
   if (x->n != dy->n || x->d != dy->d || x->h != dy->h || x->w != dy->w) return false;
   if (!chunk_ok(x, 2) || !chunk_ok(dy, 2)) return false;
-  for (const vsrk_tensor5* t : {x, dy})
-    if (t->sn < 0 || t->sd < 0 || t->sh < 0 || t->sw < 0 || (int64_t)(RW_XV + 2) * t->sw + t->c >= (1ll << 29))
+  for (const vsrk_tensor5* t : {x, dy}) {
+    const int64_t r = t->shuffle > 1 ? t->shuffle : 1;
+    if (t->sn < 0 || t->sd < 0 || t->sh < 0 || t->sw < 0 ||
+        (int64_t)(RW_XV + 2) * r * t->sw + (r - 1) * t->sh + t->c >= (1ll << 29))
       return false;
+  }
   const int64_t images = (int64_t)x->n * x->d;
   if (images <= 0 || x->h <= 0 || x->w <= 0) return false;
   const int nseg = ceil_div(x->w, RW_SEG);
@@ -411,8 +447,29 @@ int vsrk_conv_wgrad_row(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vs
   a.x = (const char*)x->ptr;
   a.dy = (const char*)dy->ptr;
   a.ws = ws;
-  a.xsn = x->sn; a.xsd = x->sd; a.xsh = x->sh; a.xsw = x->sw;
-  a.ysn = dy->sn; a.ysd = dy->sd; a.ysh = dy->sh; a.ysw = dy->sw;
+  // logical (LR-grid) strides and per-block offsets of the two operands
+  auto blocks = [](const vsrk_tensor5* t, int64_t& sh, int64_t& sw, int* off) {
+    const int r = t->shuffle > 1 ? t->shuffle : 1;
+    sh = (int64_t)r * t->sh;
+    sw = (int64_t)r * t->sw;
+    const int cph = t->c / (r * r);
+    for (int b = 0; b < t->c / 64; ++b) {
+      const int c = 64 * b, sub = c / cph, cc = c - sub * cph;
+      off[b] = (int)((sub / r) * t->sh + (sub % r) * t->sw + cc);
+    }
+  };
+  a.xsn = x->sn; a.xsd = x->sd;
+  a.ysn = dy->sn; a.ysd = dy->sd;
+  blocks(x, a.xsh, a.xsw, a.xoff);
+  blocks(dy, a.ysh, a.ysw, a.yoff);
+  const vsrk_tensor5* spt = x->shuffle > 1 ? x : (dy->shuffle > 1 ? dy : nullptr);
+  const bool spm = d->subpixel && spt;
+  a.tapm_x = spt == x;
+  if (spm) {
+    const int r = spt->shuffle, cph = spt->c / (r * r);
+    const int32_t code = d->subpixel & ~(1 << 25);  // gradients of the forward (unflipped) taps
+    for (int b = 0; b < spt->c / 64; ++b) a.tapm[b] = (uint16_t)subpixel_tapmask(code, r, 64 * b / cph);
+  }
   a.xd = x->d;
   a.H = x->h;
   a.W = x->w;
@@ -434,7 +491,7 @@ int vsrk_conv_wgrad_row(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vs
   const int grid = p.nsplit * p.ncot * p.ncic;
   vsrk_dispatch16(x->dtype, [&](auto tag) {
     using H = decltype(tag);
-    auto kern = wgrad_row_kernel<H>;
+    auto kern = spm ? wgrad_row_kernel<H, true> : wgrad_row_kernel<H, false>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, RW_LDS);
     kern<<<grid, RW_NW * 64, RW_LDS, s>>>(a);
     return 0;
