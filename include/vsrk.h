@@ -135,19 +135,25 @@ int vsrk_conv_fwd_reduce(const vsrk_conv_desc* desc, const vsrk_tensor5* x, cons
                          const float* shift, const float* mean, const float* invstd, float* out_a,
                          float* out_b, void* workspace, size_t workspace_bytes, void* stream);
 
-/* A 3x3 conv's output followed by the backward of the PReLU whose gradient
- * it is (DRF's projection chains, drf_net.py:81-102: the data gradient of a
- * ConvTranspose2d / strided Conv2d feeding the preceding conv1's PReLU):
- *   y = conv(x) * (y_fwd > 0 ? 1 : a),   *da [+]= sum_{y_fwd < 0} y * y_fwd / a^2
+/* A conv's output followed by the backward of the PReLU whose gradient it
+ * is (DRF's chains, drf_net.py:55-106: the data gradient of a projection or
+ * of a 1x1 conv feeding an earlier PReLU):
+ *   t = conv(x) [+ y if desc->accumulate]
+ *   y[c] = c >= c_lo ? t * (y_fwd > 0 ? 1 : a) : t
+ *   *da [+]= sum_{c >= c_lo, y_fwd < 0} y * y_fwd / a^2
  * with a = *desc->mask_slope and y_fwd the PReLU's forward output (y's shape
- * and strides).  The rolling 2-D kernel's forms only (3x3 pad 1 over 64-channel
- * output blocks, plain or sub-pixel views); VSRK_ERR_UNSUPPORTED otherwise
- * (the caller runs vsrk_conv_fwd + vsrk_prelu_bwd).  Fixed-order partials
- * (deterministic); workspace vsrk_conv_prelu_bwd_workspace() bytes. */
+ * and strides; only channels >= c_lo are read).  c_lo > 0 serves a consumer
+ * that owns the tail slice of a concat gradient (its last contribution is
+ * this conv).  Forms: the rolling 2-D kernel's (3x3 pad 1 over 64-channel
+ * output blocks, plain or sub-pixel views, c_lo = 0) and the staged pointwise
+ * kernel's (1x1, no bias); VSRK_ERR_UNSUPPORTED otherwise (the caller runs
+ * vsrk_conv_fwd + vsrk_prelu_bwd).  Fixed-order per-wave partials and a
+ * fixed-order final sum (deterministic); workspace
+ * vsrk_conv_prelu_bwd_workspace() bytes. */
 size_t vsrk_conv_prelu_bwd_workspace(void);
 int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* desc, const vsrk_tensor5* x, const void* w_packed,
-                            const float* bias, const vsrk_tensor5* y_fwd, const vsrk_tensor5* y, float* da,
-                            int32_t accumulate_da, void* workspace, size_t workspace_bytes, void* stream);
+                            const float* bias, const vsrk_tensor5* y_fwd, const vsrk_tensor5* y, int32_t c_lo,
+                            float* da, int32_t accumulate_da, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Tuning knob for A/B measurement: -1 (default) = bf16 fast path when
  * eligible (env VSRK_CONV_FAST=0 disables), 0 = always the generic kernel,

@@ -40,7 +40,8 @@ extern "C" int vsrk_conv_set_algo(int32_t mode) {
 extern "C" int vsrk_conv_set_path(const char* path, int32_t mode) {
   VSRK_CHECK(path, "conv_set_path: null path");
   const std::string p(path);
-  VSRK_CHECK(mode >= -1 && mode <= (p == "wgrad_row" ? 2 : 1), "conv_set_path: mode must be -1, 0 or 1 (wgrad_row: 2)");
+  VSRK_CHECK(mode >= -1 && mode <= (p == "wgrad_row" || p == "roll_wr" ? 2 : 1),
+             "conv_set_path: mode must be -1, 0 or 1 (wgrad_row, roll_wr: 2)");
   if (p == "fast") g_fast_mode = mode;
   else if (p == "thin") vsrk_g_thin_mode = mode;
   else if (p == "wgrad_pipe") vsrk_g_wgrad_pipe_mode = mode;
@@ -48,8 +49,9 @@ extern "C" int vsrk_conv_set_path(const char* path, int32_t mode) {
   else if (p == "roll") vsrk_conv_set_roll_mode(mode);
   else if (p == "wgrad_roll") vsrk_conv_set_wgrad_roll_mode(mode);
   else if (p == "wgrad_row") vsrk_conv_set_wgrad_row_mode(mode);
+  else if (p == "roll_wr") vsrk_conv_set_roll_wr_mode(mode);
   else if (p == "stencil") vsrk_conv_set_stencil_mode(mode);
-  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, pw, roll, thin, wgrad_pipe, wgrad_roll, wgrad_row, stencil)",
+  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, pw, roll, roll_wr, thin, wgrad_pipe, wgrad_roll, wgrad_row, stencil)",
                   path);
   return VSRK_OK;
 }

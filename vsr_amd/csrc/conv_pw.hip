@@ -34,6 +34,10 @@ namespace {
 using namespace vsrk_conv;
 
 constexpr int PW_THR = 256;  // 4 waves, one per SIMD
+#ifndef PW_EIN_EARLY
+#define PW_EIN_EARLY 1
+#endif
+enum { EIN_GEN = 1, EIN_ACC = 2, EIN_PB = 3, EIN_PBACC = 4 };  // staged kernel store-pass forms
 constexpr int PW_KP = 64;    // wgrad voxels per stage
 #ifndef PW_NT
 #define PW_NT 2  // non-temporal output stores of the staged kernel (DUF 75.8 -> 75.4 ms, profiles/r4_pw_nt_ab.txt); 0 for A/B
@@ -158,6 +162,13 @@ struct PwArgs {  // 16-bit tensors of one type H (bf16 / fp16)
   FastDiv fd;                             // division by dhw
   int cin, cout, ci_pad, co_rows;
   int prologue, act, accumulate, has_mask;
+  // PBWD (EIN form): the PReLU backward of the output's consumer applied
+  // after the accumulate, on output channels >= pm_lo (a consumer that
+  // owns the tail slice of a concat gradient): dy' = (conv [+ dy]) *
+  // (msk > 0 ? 1 : slope), msk = that PReLU's output; the slope gradient
+  // sum_{msk<0} dy' msk as per-lane partials, slab [block y][block x][wave][lane]
+  int pbwd, pm_lo;
+  double* slope_part;  // [block y][block x][wave] partials of the slope gradient
   float out_scale;
   int ntiles;  // tiles of 32*M voxels
   int ablate;  // A/B knob (VSRK_PW_ABLATE): 1 = no stores, 2 = no MFMA, 4 = no loads (staged)
@@ -370,7 +381,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_kernel(PwArgs a) {
 // separate apply's; k1 = gamma * invstd is bn_finalize's scale, bn.hip:193),
 // computed on the 16-byte row chunks between the coalesced loads and the LDS
 // put, and stored once to xo for the weight gradient.
-template <int NCB, int NKB, int M, bool PRO, bool AL, int ACT, bool EIN, typename H, int RED = 0, bool BNB = false>
+template <int NCB, int NKB, int M, bool PRO, bool AL, int ACT, int EIN, typename H, int RED = 0, bool BNB = false>
 __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
   const H* aX = reinterpret_cast<const H*>(a.x);
   H* aY = reinterpret_cast<H*>(a.y);
@@ -433,6 +444,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   const float osc = a.out_scale;
   const float pslope = ACT == VSRK_ACT_PRELU ? *a.act_param : 0.f;
+  float sacc = 0.f;  // PBWD: this lane's slope-gradient partial
   // fused reduction: this lane's fixed 8-channel column and its constants
   constexpr int ROCPR = COP / 8;
   constexpr int RSTEP = 64 / ROCPR > 0 ? 64 / ROCPR : 1;
@@ -531,6 +543,39 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
     }
   };
 
+  constexpr int EIN_NOK = ROWS * (COP / 8) / 64;  // store-pass row chunks per lane
+  // EIN forms: 1 = generic (runtime flags: mask, accumulate, PBWD on the
+  // channels >= pm_lo); compile-time and branch-free: EIN_ACC (accumulate),
+  // EIN_PB (PBWD), EIN_PBACC (both).  The generic store pass carried ~3.5 K
+  // extra instructions per tile (divergent per-chunk branches): 2.2x the plain
+  // kernel's time at DRF's 64 -> 256 data gradients.
+  const bool f_mask = EIN == 1 ? a.has_mask != 0 : false;
+  const bool f_acc = EIN == 1 ? a.accumulate != 0 : (EIN == EIN_ACC || EIN == EIN_PBACC);
+  const bool f_pb = EIN == 1 ? a.pbwd != 0 : (EIN == EIN_PB || EIN == EIN_PBACC);
+  auto ein_load = [&](int tile, uint4 (&em)[EIN ? EIN_NOK : 1], uint4 (&ey)[EIN ? EIN_NOK : 1])
+                      __attribute__((always_inline)) {
+    if constexpr (EIN) {
+      constexpr int OCPR = COP / 8;
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const int v0 = tile * ROWS;
+      const TileBase tb = tile_base(v0, a.fd);
+      const Rsrc ry = rsrc_at(aY + (int64_t)tb.n0 * a.ysn);
+      const Rsrc rm = rsrc_at(reinterpret_cast<const H*>(a.msk ? a.msk : a.y) + (int64_t)tb.n0 * a.msn);
+#pragma unroll
+      for (int k = 0; k < EIN_NOK; ++k) {
+        const int i = ln + 64 * k, row = i / OCPR, c = 8 * (i % OCPR);
+        const bool ok = co0 + c < a.cout;
+        if (EIN == 1) {
+          if (f_mask || (f_pb && co0 + c >= a.pm_lo))
+            em[k] = bload16(rm, ok ? row_off(tb, row, v0, a.msn, a.msw) + 2 * (co0 + c) : PW_OOB);
+        } else if (f_pb) {  // branch-free: chunks below pm_lo read nothing (out-of-range offset) and see m = 0
+          em[k] = bload16(rm, ok && co0 + c >= a.pm_lo ? row_off(tb, row, v0, a.msn, a.msw) + 2 * (co0 + c) : PW_OOB);
+        }
+        if (f_acc) ey[k] = bload16(ry, ok ? row_off(tb, row, v0, a.ysn, a.ysw) + 2 * (co0 + c) : PW_OOB);
+      }
+    }
+  };
   uint4 rg[NCK], rgq[NQK];
   int t = blockIdx.x * (PW_THR / 64) + wv;
   if (t < a.ntiles) load(t, rg, rgq);
@@ -554,6 +599,12 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
     };
     if constexpr (RED == 2 && PW_BXPRE) load_bx();
     if (tn < a.ntiles) load(tn, rg, rgq);  // in flight during this tile's MFMAs and stores
+    // EIN: the store pass's mask / accumulate operands of this tile, issued
+    // before its MFMAs (PW_EIN_EARLY) so their latency hides under them; issued
+    // at the store pass they made an accumulate data gradient 2.2x the plain one
+    // (DRF 64 -> 256 at 512^2: 312 vs 143 us, r5 tools/diag/pw_pbwd_micro.py)
+    uint4 em[EIN ? EIN_NOK : 1], ey[EIN ? EIN_NOK : 1];
+    if constexpr (EIN && PW_EIN_EARLY) ein_load(t, em, ey);
 
     f32x16 acc[M][NCB];
 #pragma unroll
@@ -677,18 +728,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
       static_assert(NOK >= 1 && ROWS * OCPR % 64 == 0, "whole row chunks per lane");
       int ln = lane;
       asm volatile("" : "+v"(ln));
-      // EIN operands of every chunk first (all loads in flight together)
-      uint4 em[EIN ? NOK : 1], ey[EIN ? NOK : 1];
-      if constexpr (EIN) {
-        const Rsrc rm = rsrc_at(reinterpret_cast<const H*>(a.has_mask ? a.msk : a.y) + (int64_t)tb.n0 * a.msn);
-#pragma unroll
-        for (int k = 0; k < NOK; ++k) {
-          const int i = ln + 64 * k, row = i / OCPR, c = 8 * (i % OCPR);
-          const bool ok = co0 + c < a.cout;
-          if (a.has_mask) em[k] = bload16(rm, ok ? row_off(tb, row, v0, a.msn, a.msw) + 2 * (co0 + c) : PW_OOB);
-          if (a.accumulate) ey[k] = bload16(ry, ok ? row_off(tb, row, v0, a.ysn, a.ysw) + 2 * (co0 + c) : PW_OOB);
-        }
-      }
+      if constexpr (EIN && !PW_EIN_EARLY) ein_load(t, em, ey);  // every chunk's operands in flight together
       const float mslope = (EIN && a.mask_slope) ? *a.mask_slope : 0.f;
 #pragma unroll
       for (int k = 0; k < NOK; ++k) {
@@ -697,19 +737,42 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
         if constexpr (EIN) {
           float o[8];
           Chunk<H>::unpack(v, o);
-          if (a.has_mask) {
+          if (f_mask) {
             float m[8];
             Chunk<H>::unpack(em[k], m);
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[e] = mask_apply(m[e], o[e], mslope);
           }
-          if (a.accumulate) {
+          if (f_acc) {
             float yo[8];
             Chunk<H>::unpack(ey[k], yo);
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[e] += yo[e];
           }
           v = Chunk<H>::pack(o);
+          if (EIN != 1 && f_pb) {
+            const bool tail = co0 + c >= a.pm_lo;
+            float m[8], tr[8];
+            Chunk<H>::unpack(em[k], m);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = (tail && !(m[e] > 0.f)) ? mslope * o[e] : o[e];
+            v = Chunk<H>::pack(o);
+            Chunk<H>::unpack(v, tr);  // the stored (rounded) values, as prelu_bwd reads them
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sacc = fmaf(m[e] < 0.f ? tr[e] : 0.f, m[e], sacc);  // m = 0 off the tail
+          } else if (f_pb && co0 + c >= a.pm_lo) {
+            float m[8];
+            Chunk<H>::unpack(em[k], m);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = m[e] > 0.f ? o[e] : mslope * o[e];
+            v = Chunk<H>::pack(o);
+            float tr[8];
+            Chunk<H>::unpack(v, tr);  // the stored (rounded) values, as prelu_bwd reads them
+            // (out-of-range rows load zeros: m = 0 adds nothing)
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (m[e] < 0.f) sacc = fmaf(tr[e], m[e], sacc);
+          }
         }
         const uint32_t off = row_off(tb, row, v0, a.ysn, a.ysw);
         if (!(a.ablate & 1))
@@ -718,6 +781,13 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
       }
     }
     t = tn;
+  }
+  if constexpr (EIN) {
+    if (f_pb) {
+      const double wsum = vsrk_wave_sum((double)sacc);
+      if (lane == 0) a.slope_part[(blockIdx.y * gridDim.x + blockIdx.x) * (PW_THR / 64) + wave] = wsum;
+      return;
+    }
   }
   if constexpr (RED != 0) {
     float* o = a.red_ws + ((((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * (PW_THR / 64) + wave) * 64 + lane) * 16;
@@ -1069,7 +1139,7 @@ static bool launch_fwd_staged(const PwArgs& a, int grid, int nchunk, bool pro, h
     staged = (e && e[0] == '0') ? 0 : 1;
   }
   if (!staged || a.cout % 8 != 0) return false;
-  const bool ein = a.has_mask || a.accumulate;
+  const bool ein = a.has_mask || a.accumulate || a.pbwd;
   if (ein && (pro || a.act != VSRK_ACT_NONE)) return false;  // data gradients: no prologue / activation
   if (pro && a.act == VSRK_ACT_PRELU) return false;
   constexpr int RW = CIP > COP ? CIP : COP;
@@ -1079,8 +1149,22 @@ static bool launch_fwd_staged(const PwArgs& a, int grid, int nchunk, bool pro, h
   using K = void (*)(PwArgs);
   K kern;
   if (ein) {
-    kern = al ? pw_fwd_staged_kernel<NCB, NKB, M, false, true, 0, true, H>
-              : pw_fwd_staged_kernel<NCB, NKB, M, false, false, 0, true, H>;
+    kern = al ? pw_fwd_staged_kernel<NCB, NKB, M, false, true, 0, EIN_GEN, H>
+              : pw_fwd_staged_kernel<NCB, NKB, M, false, false, 0, EIN_GEN, H>;
+    if constexpr (NKB == 2) {  // DRF's 64-input-channel data gradients: the branch-free forms
+      if (!a.has_mask && (a.accumulate || a.pbwd)) {
+        const int mode = a.pbwd ? (a.accumulate ? EIN_PBACC : EIN_PB) : EIN_ACC;
+        if (mode == EIN_ACC)
+          kern = al ? pw_fwd_staged_kernel<NCB, NKB, M, false, true, 0, EIN_ACC, H>
+                    : pw_fwd_staged_kernel<NCB, NKB, M, false, false, 0, EIN_ACC, H>;
+        else if (mode == EIN_PB)
+          kern = al ? pw_fwd_staged_kernel<NCB, NKB, M, false, true, 0, EIN_PB, H>
+                    : pw_fwd_staged_kernel<NCB, NKB, M, false, false, 0, EIN_PB, H>;
+        else
+          kern = al ? pw_fwd_staged_kernel<NCB, NKB, M, false, true, 0, EIN_PBACC, H>
+                    : pw_fwd_staged_kernel<NCB, NKB, M, false, false, 0, EIN_PBACC, H>;
+      }
+    }
   } else if (a.act == VSRK_ACT_PRELU) {
     kern = al ? pw_fwd_staged_kernel<NCB, NKB, M, false, true, VSRK_ACT_PRELU, false, H>
               : pw_fwd_staged_kernel<NCB, NKB, M, false, false, VSRK_ACT_PRELU, false, H>;
@@ -1190,10 +1274,44 @@ static bool pw_fill_args(PwArgs& a, const vsrk_conv_desc* d, const vsrk_tensor5*
   return true;
 }
 
+namespace {
+struct PwPbwd {  // the PBWD form (see PwArgs::pbwd)
+  int c_lo;
+  const vsrk_slope_out* out;
+};
+}  // namespace
+
+static int fwd_pw_impl(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                       const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
+                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s, const PwPbwd* pb);
+
 // 1 = launched, 0 = not eligible (caller uses the tile kernels), <0 = -status.
 int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
                      const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                      const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s) {
+  return fwd_pw_impl(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s, nullptr);
+}
+
+// The data gradient of a pointwise conv with its consumer's PReLU backward
+// after the accumulate on output channels >= c_lo (mask = that PReLU's output,
+// y's geometry): 1 = launched (*nparts slope partials in ws), 0 = not eligible.
+int vsrk_conv_fwd_pw_pbwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed,
+                          const vsrk_tensor5* mask, const vsrk_tensor5* y, int c_lo, const vsrk_slope_out* slope,
+                          hipStream_t s) {
+  if (!mask || !d->mask_slope || d->prologue || d->act != VSRK_ACT_NONE || d->out_scale != 1.f) return 0;
+  if (c_lo < 0 || c_lo >= y->c || c_lo % 8) return 0;
+  if (mask->shuffle > 1 || y->shuffle > 1) return 0;
+  vsrk_conv_desc dd = *d;
+  PwPbwd pb{c_lo, slope};
+  return fwd_pw_impl(&dd, x, w_packed, nullptr, nullptr, nullptr, nullptr, mask, y, s, &pb);
+}
+
+// grid <= CUs, <= 2 output chunks, one partial per wave
+size_t vsrk_pw_pbwd_ws_bytes() { return (size_t)pw_num_cus() * 2 * (PW_THR / 64) * sizeof(double); }
+
+static int fwd_pw_impl(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                       const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
+                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s, const PwPbwd* pb) {
   if (!pw_enabled()) return 0;
   if (!vsrk_is16(x->dtype) || y->dtype != x->dtype) return 0;
   if (d->kd != 1 || d->kh != 1 || d->kw != 1 || d->pd || d->ph || d->pw) return 0;
@@ -1219,14 +1337,30 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
   const int nchunk = narrow ? 1 : cop_total / cip;
   PwArgs a;
   if (!pw_fill_args(a, d, x, w_packed, bias, pro_scale, pro_shift, mask, y, cip)) return 0;
+  if (pb) {  // the mask operand is the PReLU output read after the accumulate
+    a.has_mask = 0;
+    a.pbwd = 1;
+    a.pm_lo = pb->c_lo;
+    a.slope_part = pb->out->part;
+    *pb->out->nparts = 0;
+  }
   if (a.nvox == 0) return 1;
   const bool pro = d->prologue != VSRK_PRO_NONE;
+  // PBWD: the staged kernel only, its grid's partials must fit the workspace
+  auto pb_fits = [&](int grid, int nchunk) {
+    if (!pb) return true;
+    const size_t n = (size_t)grid * nchunk * (PW_THR / 64);
+    if (n > pb->out->cap) return false;
+    *pb->out->nparts = (int)n;
+    return true;
+  };
   if (narrow) {
     bool ok = false;
     auto go = [&](auto ncb_c, auto nkb_c) {
       constexpr int NC = decltype(ncb_c)::value, NK = decltype(nkb_c)::value;
       constexpr int M = pw_m<NK>() * NC <= 8 ? pw_m<NK>() : (8 / NC > 0 ? 8 / NC : 1);  // <= 128 accumulators
       a.ntiles = ceil_div(a.nvox, 32 * M);
+      if (!pb_fits(pw_grid(a.ntiles), 1)) return;
       vsrk_dispatch16(x->dtype, [&](auto tag) {
         ok = launch_fwd_staged<NC, NK, M, decltype(tag)>(a, pw_grid(a.ntiles), 1, pro, s);
         return 0;
@@ -1242,6 +1376,31 @@ int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void*
     else if (narrow == 6 && ncb == 2) go(std::integral_constant<int, 6>{}, I2{});
     else if (narrow == 8 && ncb == 2) go(std::integral_constant<int, 8>{}, I2{});
     else return 0;
+    if (!ok) return 0;
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      vsrk_set_error("conv_fwd_pw: launch failed: %s", hipGetErrorString(e));
+      return -(int)VSRK_ERR_LAUNCH;
+    }
+    return 1;
+  }
+  if (pb) {  // square forms: the staged kernel, NCB <= 7 (one launch per CIP-channel chunk)
+    bool ok = false;
+    switch (ncb) {
+#define PW_PB_CASE(N)                                                                              \
+  case N:                                                                                          \
+    a.ntiles = ceil_div(a.nvox, 32 * pw_m<N>());                                                   \
+    if (pb_fits(pw_grid(a.ntiles), nchunk))                                                        \
+      vsrk_dispatch16(x->dtype, [&](auto tag) {                                                    \
+        ok = launch_fwd_staged<N, N, pw_m<N>(), decltype(tag)>(a, pw_grid(a.ntiles), nchunk, pro, s); \
+        return 0;                                                                                  \
+      });                                                                                          \
+    break;
+      PW_PB_CASE(2) PW_PB_CASE(3) PW_PB_CASE(4) PW_PB_CASE(5) PW_PB_CASE(6) PW_PB_CASE(7)
+#undef PW_PB_CASE
+      default:
+        break;
+    }
     if (!ok) return 0;
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -1293,8 +1452,7 @@ static int fwd_reduce_impl(const vsrk_conv_desc* d, const vsrk_tensor5* x, const
     VSRK_CHECK(bnx && scale && shift && mean && invstd, "conv_fwd_reduce: mode 2 needs bnx and the BN constants");
     VSRK_CHECK(workspace, "conv_fwd_reduce: null workspace");
     vsrk_roll_bnred r{bnx, scale, shift, mean, invstd, (float*)workspace, workspace_bytes / sizeof(float), 0, 0};
-    const int rc = vsrk_conv_fwd_roll(d, x, w_packed, bias, nullptr, nullptr, nullptr, nullptr, y, s, nullptr,
-                                      nullptr, &r);
+    const int rc = vsrk_conv_fwd_roll(d, x, w_packed, bias, nullptr, nullptr, nullptr, nullptr, y, s, nullptr, &r);
     if (rc == 0) return VSRK_ERR_UNSUPPORTED;
     if (rc < 0) return -rc;
     if (r.ntiles == 0) {

@@ -75,16 +75,9 @@ constexpr int RNSLOT = 3;
 #ifndef ROLL_LEAN
 #define ROLL_LEAN 1
 #endif
-// ROLL_PFASM (default 0): the epilogue operand prefetch as inline-asm loads
-// the compiler cannot see.  Their destination registers then look ready at
-// once, so nothing stops the register allocator from copying or re-using
-// them before the data lands (round 4: a restructured epilogue read stale
-// residual / mask operands).  Default: ordinary loads, which the compiler
-// waits for before their first use -- at the flush, where that wait may
-// also drain the next stage's pieces (issued a stage earlier).
-#ifndef ROLL_PFASM
-#define ROLL_PFASM 0
-#endif
+// (The epilogue operand prefetch is a plain compiler-visible load; round 4's
+// inline-asm variant, whose destination registers the compiler could re-use
+// before the data landed, is gone.)
 
 
 // Geometry of the two forms.  KD = 3, NT = 1: Conv3d 3x3x3, one 32-channel
@@ -121,7 +114,9 @@ struct RollGeo {
 // [relu | prelu] [* (mask > 0)] [+ residual] [+ out]
 // RE_PMASK: the PReLU backward of the output's consumer fused in (mask = the
 // PReLU's forward output at y's element offsets; * a where it is <= 0) with
-// per-lane partials of the slope gradient (drf_net.py:56-106 PReLUs)
+// per-lane partials of the slope gradient (drf_net.py:56-106 PReLUs);
+// with RE_ACC the mask applies to the accumulated sum (out + conv: the
+// consumer's gradient is complete only after this last contribution)
 // RE_BNRED (3-D form): the reduce half of the BN+ReLU backward whose dz this
 // data gradient is (duf_net.py:198-203: bn2 before conv2) fused into the
 // epilogue: per tile and wave, (sum dy', sum dy' xhat) of its 32 channels
@@ -172,7 +167,7 @@ struct RollArgs {
   const float* act_param;
   int prio;  // A/B knob (VSRK_ROLL_PRIO=1): s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD)
   const float* mask_slope;  // RE_PMASK: the PReLU slope a (device scalar)
-  float* slope_ws;          // RE_PMASK: [block][wave][lane] partials
+  double* slope_part;       // RE_PMASK: [block][wave] partials of the slope gradient
   // RE_BNRED: the BN input (y's geometry and strides), its per-channel
   // constants and the [tile][wave][2 halves][16 sum + 16 sum-xhat] slab
   const char* bnx;
@@ -448,8 +443,8 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // channels (16 bytes) 8 (l & 3) .. +7 of the block of voxel (l >> 2) + 16 k,
   // a slice's last stages ahead of its flush.  The stage waits of the main
   // loop count them (see pf_hold) and retire them before the flush; as
-  // ordinary loads (ROLL_PFASM 0) the compiler also waits for them itself
-  // before their first use.
+  // ordinary loads the compiler also waits for them itself before their
+  // first use.
   typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
   typedef u32x4_t PreT[PREF ? RMS : 1][PREF ? NT : 1][2];
   PreT pre;
@@ -471,10 +466,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) {
             const void* src = ok ? (const void*)(pp + nt * 32) : (const void*)zp;
-            if constexpr (ROLL_PFASM)
-              asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst[ms][nt][k]) : "v"(src) : "memory");
-            else
-              dst[ms][nt][k] = *reinterpret_cast<const u32x4_t*>(src);
+            dst[ms][nt][k] = *reinterpret_cast<const u32x4_t*>(src);
           }
         }
       }
@@ -579,6 +571,10 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   const float pslope = (EM & RE_PRELU) ? *a.act_param : 0.f;
   const float mslope = (EM & RE_PMASK) ? *a.mask_slope : 0.f;
   float sacc = 0.f;  // RE_PMASK: this lane's sum_{mask < 0} out * mask
+  auto slope_out = [&](float v) __attribute__((always_inline)) {  // the wave's partial, at its end
+    const double wsum = vsrk_wave_sum((double)v);
+    if (lane == 0) a.slope_part[blockIdx.x * RNW + wave] = wsum;
+  };
   // Transposed epilogue (output block nt of depth dz; both forms): per row ms
   // the wave parks its fp32 accumulators (32 voxels x 32 channels) in LDS and
   // reads them back as 8 consecutive channels of one voxel per lane, so every
@@ -704,6 +700,12 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
             for (int e = 0; e < 8; ++e) t[e] = m[e] > 0.f ? t[e] : 0.f;
           }
           if constexpr (EM & RE_PMASK) {
+            if constexpr (EM & RE_ACC) {  // the consumer's PReLU backward sees the whole sum: after the accumulate
+              float o[8];
+              Chunk<H>::unpack(*reinterpret_cast<const uint4*>(yp), o);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) t[e] += o[e];
+            }
             const uint4 mv = *reinterpret_cast<const uint4*>(reinterpret_cast<const H*>(a.msk.ptr) +
                                                              (yp - reinterpret_cast<H*>(a.y.ptr)));
             float m[8];
@@ -732,7 +734,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) t[e] += rr[e];
           }
-          if constexpr (EM & RE_ACC) {
+          if constexpr ((EM & RE_ACC) && !(EM & RE_PMASK)) {
             float o[8];
             Chunk<H>::unpack(*reinterpret_cast<const uint4*>(yp), o);
 #pragma unroll
@@ -819,8 +821,8 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   auto stamp = [&]() __attribute__((always_inline)) {};
 #endif
   int t = t_lo + jb;
-  if (t >= t_hi) {
-    if constexpr (EM & RE_PMASK) a.slope_ws[(blockIdx.x * RNW + wave) * 64 + lane] = 0.f;
+  if (t >= t_hi) {  // (workgroup-uniform) no tile: a zero partial, still counted
+    if constexpr (EM & RE_PMASK) slope_out(0.f);
     return;
   }
   Walk nx;
@@ -984,7 +986,6 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   roll_wait_vmcnt<0>();  // the last stage's prefetch
   if (ppre) settle();
   flush(ptl, pdi, true, ppre, fscr);
-  if constexpr (EM & RE_PMASK) a.slope_ws[(blockIdx.x * RNW + wave) * 64 + lane] = sacc;
 #ifdef ROLL_STAMP
   if (blockIdx.x < 16 && (wave == 0 || wave == 4)) {
     unsigned* o = g_roll_stamp + (blockIdx.x * 2 + (wave >> 2)) * 128;
@@ -992,6 +993,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
     o[64 + lane] = stv1;
   }
 #endif
+  if constexpr (EM & RE_PMASK) slope_out(sacc);
 }
 
 // Channel c of the fused BN+ReLU backward reduce: the (tile, wave) partials
@@ -1044,49 +1046,11 @@ __global__ __launch_bounds__(256) void roll_bnred_final_kernel(const float* __re
   }
 }
 
-// da [+]= (sum of the partials, fixed order, double) / a^2: the PReLU slope
-// gradient sum_{y<0} dx * y / a^2 as prelu_bwd_kernel + prelu_final_kernel
-// (drf.hip) compute it
-// n is a multiple of 4 (RNW * 64 partials per block). One workgroup of 1024
-// lanes, eight independent 16-byte loads in flight per lane before the adds:
-// the partials are latency-bound, not bandwidth-bound (a 256-lane serial loop
-// over 64 K floats ran ~100 us).
-__global__ __launch_bounds__(1024) void roll_slope_final_kernel(const float* __restrict__ part, int n,
-                                                                const float* __restrict__ a, float* __restrict__ da,
-                                                                int accumulate) {
-  constexpr int U = 8;
-  __shared__ double sh[1024];
-  const float4* p4 = reinterpret_cast<const float4*>(part);
-  const int n4 = n >> 2;
-  double s = 0.0;
-  for (int base = threadIdx.x; base < n4; base += 1024 * U) {
-    float4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = base + u * 1024;
-      v[u] = i < n4 ? p4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) s += ((double)v[u].x + (double)v[u].y) + ((double)v[u].z + (double)v[u].w);
-  }
-  sh[threadIdx.x] = s;
-  __syncthreads();
-  for (int k = 512; k > 0; k >>= 1) {
-    if (threadIdx.x < k) sh[threadIdx.x] += sh[threadIdx.x + k];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const double av = (double)*a;
-    // The tape holds PReLU outputs only: y < 0 marks x < 0 only while a > 0.
-    // A slope <= 0 makes the output-based gradient ambiguous, so it poisons
-    // da with NaN (a loud failure in the optimizer step, never a silently
-    // wrong gradient); nn.PReLU starts at 0.2 (drf_net.py:56).
-    const float v = av > 0.0 ? (float)(sh[0] / (av * av)) : __builtin_nanf("");
-    *da = accumulate ? *da + v : v;
-  }
-}
 
 int g_roll_mode = -1;  // -1: from VSRK_CONV_ROLL (unset: 2), 0 off, 1 forced on, 2 automatic
+// resident weights (WR): -1 from VSRK_ROLL_WRES (unset: 1), 0 off, 1 where
+// faster, 2 also with the prefetched residual / mask epilogue (tests)
+int g_roll_wr_mode = -1;
 
 int roll_num_cus() {
   static int n = 0;
@@ -1119,15 +1083,17 @@ extern "C" int vsrk_conv_set_roll_depth(int32_t depths) {
   return VSRK_OK;
 }
 
+void vsrk_conv_set_roll_wr_mode(int mode) { g_roll_wr_mode = mode; }
+
 void vsrk_conv_set_roll_mode(int mode) { g_roll_mode = mode; }
 
 // 1 = launched, 0 = not eligible, < 0 = -(error status)
-size_t vsrk_roll_slope_ws_floats() { return (size_t)roll_num_cus() * RNW * 64; }
+size_t vsrk_roll_slope_ws_bytes() { return (size_t)roll_num_cus() * RNW * sizeof(double); }
 
 int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
-                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s, float* slope_ws,
-                       int* slope_blocks, vsrk_roll_bnred* bnred) {
+                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s, const vsrk_slope_out* slope,
+                       vsrk_roll_bnred* bnred) {
   if (g_roll_mode < 0) {
     const char* e = getenv("VSRK_CONV_ROLL");
     g_roll_mode = !e ? 2 : (e[0] == '0' ? 0 : 1);
@@ -1139,15 +1105,16 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   // depth-1 slices with 64-channel output blocks (cout a multiple of 64)
   const bool k3 = d->kd == 3;
   if (!k3 && !(d->kd == 1 && d->pd == 0 && y->c % 64 == 0)) return 0;
-  // PReLU-backward mask (slope_ws): the mask has y's geometry and strides
-  const bool pmask = slope_ws != nullptr;
+  // PReLU-backward mask (slope): the mask has y's geometry and strides
+  const bool pmask = slope != nullptr;
   if ((d->bias_perm_r > 1 && (y->shuffle != d->bias_perm_r || y->c % (d->bias_perm_r * d->bias_perm_r))) ||
       (d->mask_slope && !pmask))
     return 0;
   if (pmask) {
     if (!mask || !d->mask_slope || residual || d->kd != 1 || d->prologue) return 0;
     if (mask->dtype != y->dtype || mask->shuffle != y->shuffle || mask->n != y->n || mask->d != y->d ||
-        mask->h != y->h || mask->w != y->w || mask->c != y->c || mask->sn != y->sn || mask->sd != y->sd ||
+        mask->h != y->h || mask->w != y->w || mask->c != y->c || mask->sn != y->sn ||
+        (y->d > 1 && mask->sd != y->sd) ||
         mask->sh != y->sh || mask->sw != y->sw)
       return 0;
   }
@@ -1275,20 +1242,24 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   // -- EDSR's 64 -> 64 body convs -- or (3-D) whole-depth tiles, where a
   // reload per tile is amortised over nsl x nchunk stages (DUF's data
   // gradients 32 -> F).  VSRK_ROLL_WRES=0 turns it off (A/B).
-  static int wres_mode = -1;
-  if (wres_mode < 0) {
+  if (g_roll_wr_mode < 0) {
     const char* e = getenv("VSRK_ROLL_WRES");
-    wres_mode = (e && e[0] == '0') ? 0 : 1;
+    g_roll_wr_mode = (e && e[0] == '0') ? 0 : 1;
   }
+  const int wres_mode = g_roll_wr_mode;
   const size_t nb = k3 ? RollGeo<3, 1>::NB : RollGeo<1, 2>::NB;
   const size_t wbytes = (size_t)a.nchunk * nb * 1024;
   const size_t tables = (size_t)a.cout_pad * 4 + (d->prologue || bnred ? 2 * (size_t)a.cin_pad * 4 : 0) +
                         (bnred ? 4 * (size_t)a.cout_pad * 4 : 0);
   const size_t wslot = k3 ? RollGeo<3, 1, 1>::SLOT : RollGeo<1, 2, 1>::SLOT;
-  // (2-D: not with a prefetched residual / mask operand -- those epilogues
-  // give wrong results with the two-pass park of the 24 KB WR slots, cause
-  // not found yet; tests/test_roll_gpu.py res / mask cases)
-  const bool pref2d = !k3 && ((residual != nullptr) != (mask != nullptr && !pmask)) && !d->accumulate;
+  // (2-D: not with a prefetched residual / mask operand unless forced (mode
+  // 2): correct -- tests/test_roll_gpu.py compares the forced form bitwise
+  // with the streamed one; round 4's wrong results came with the inline-asm
+  // prefetch, whose registers the compiler could re-use before the data
+  // landed, since removed -- but slower: EDSR res 129 -> 146 us, mask
+  // 147 -> 163 us per launch (profiles/r5_roll_wr_prefetch_ab.txt))
+  const bool pref2d =
+      wres_mode != 2 && !k3 && ((residual != nullptr) != (mask != nullptr && !pmask)) && !d->accumulate;
   const bool wr = wres_mode && sp == SP_NONE && !d->prologue && wbytes <= 80 * 1024 && !pref2d &&
                   (k3 ? dzc == y->d : ntn == 1) && (size_t)RNSLOT * wslot + wbytes + tables <= 160 * 1024;
   const size_t slot = wr ? wslot : (k3 ? RollGeo<3, 1>::SLOT : RollGeo<1, 2>::SLOT);
@@ -1311,8 +1282,11 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   const int em = (residual ? RE_RES : 0) | (mask ? (pmask ? RE_PMASK : RE_MASK) : 0) | (d->accumulate ? RE_ACC : 0) |
                  (relu ? RE_RELU : 0) | (d->act == VSRK_ACT_PRELU ? RE_PRELU : 0);
   a.mask_slope = d->mask_slope;
-  a.slope_ws = slope_ws;
-  if (slope_blocks) *slope_blocks = grid;
+  if (pmask) {
+    if ((size_t)grid * RNW > slope->cap) return 0;
+    a.slope_part = slope->part;
+    *slope->nparts = grid * RNW;
+  }
   int rc = vsrk_dispatch16(x->dtype, [&](auto tag) {
     using H = decltype(tag);
     if (k3) {
@@ -1339,6 +1313,7 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
         case RE_PRELU: return launch_roll<1, 2, 0, RE_PRELU, SP_X, H>(a, lds, grid, s);
         case RE_ACC: return launch_roll<1, 2, 0, RE_ACC, SP_X, H>(a, lds, grid, s);
         case RE_PMASK: return launch_roll<1, 2, 0, RE_PMASK, SP_X, H>(a, lds, grid, s);
+        case RE_PMASK | RE_ACC: return launch_roll<1, 2, 0, RE_PMASK | RE_ACC, SP_X, H>(a, lds, grid, s);
         default: return (int)VSRK_ERR_UNSUPPORTED;
       }
     }
@@ -1348,6 +1323,7 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
         case RE_PRELU: return launch_roll<1, 2, 0, RE_PRELU, SP_Y, H>(a, lds, grid, s);
         case RE_ACC: return launch_roll<1, 2, 0, RE_ACC, SP_Y, H>(a, lds, grid, s);
         case RE_PMASK: return launch_roll<1, 2, 0, RE_PMASK, SP_Y, H>(a, lds, grid, s);
+        case RE_PMASK | RE_ACC: return launch_roll<1, 2, 0, RE_PMASK | RE_ACC, SP_Y, H>(a, lds, grid, s);
         default: return (int)VSRK_ERR_UNSUPPORTED;
       }
     }
@@ -1380,22 +1356,38 @@ extern "C" int vsrk_roll_stamps(unsigned* dst) {
 }
 #endif
 
-extern "C" size_t vsrk_conv_prelu_bwd_workspace(void) { return vsrk_roll_slope_ws_floats() * sizeof(float); }
+extern "C" size_t vsrk_conv_prelu_bwd_workspace(void) {
+  return std::max(vsrk_roll_slope_ws_bytes(), vsrk_pw_pbwd_ws_bytes());
+}
 
 extern "C" int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed,
-                                       const float* bias, const vsrk_tensor5* y_fwd, const vsrk_tensor5* y, float* da,
-                                       int32_t accumulate_da, void* workspace, size_t workspace_bytes, void* stream) {
+                                       const float* bias, const vsrk_tensor5* y_fwd, const vsrk_tensor5* y,
+                                       int32_t c_lo, float* da, int32_t accumulate_da, void* workspace,
+                                       size_t workspace_bytes, void* stream) {
   VSRK_CHECK(d && x && y && y_fwd && w_packed && da && d->mask_slope, "conv_fwd_prelu_bwd: null argument");
   VSRK_CHECK(workspace && workspace_bytes >= vsrk_conv_prelu_bwd_workspace(),
              "conv_fwd_prelu_bwd: workspace %zu < %zu bytes", workspace_bytes, vsrk_conv_prelu_bwd_workspace());
   VSRK_CHECK(((uintptr_t)workspace & 15) == 0, "conv_fwd_prelu_bwd: workspace must be 16-byte aligned");
+  VSRK_CHECK(c_lo >= 0 && c_lo < y->c, "conv_fwd_prelu_bwd: c_lo %d outside [0, %d)", c_lo, y->c);
   hipStream_t s = (hipStream_t)stream;
-  int nb = 0;
-  const int rc = vsrk_conv_fwd_roll(d, x, w_packed, bias, nullptr, nullptr, nullptr, y_fwd, y, s, (float*)workspace, &nb);
+  if ((int64_t)y->n * y->d * y->h * y->w == 0) {  // nothing to launch: no slope gradient
+    if (!accumulate_da) (void)hipMemsetAsync(da, 0, sizeof(float), s);
+    return VSRK_OK;
+  }
+  int nparts = 0;
+  const vsrk_slope_out so{(double*)workspace, workspace_bytes / sizeof(double), &nparts};
+  int rc;
+  if (d->kd == 1 && d->kh == 1 && d->kw == 1) {
+    // pointwise: the staged kernel's post-accumulate form, any channel tail
+    if (bias) return VSRK_ERR_UNSUPPORTED;
+    rc = vsrk_conv_fwd_pw_pbwd(d, x, w_packed, y_fwd, y, c_lo, &so, s);
+  } else {
+    if (c_lo != 0) return VSRK_ERR_UNSUPPORTED;  // the rolling kernel masks every output channel
+    rc = vsrk_conv_fwd_roll(d, x, w_packed, bias, nullptr, nullptr, nullptr, y_fwd, y, s, &so);
+  }
   if (rc == 0) return VSRK_ERR_UNSUPPORTED;
   if (rc < 0) return -rc;
-  roll_slope_final_kernel<<<1, 1024, 0, s>>>((const float*)workspace, nb * RNW * 64, d->mask_slope, da,
-                                            accumulate_da);
+  vsrk_slope_final((const double*)workspace, nparts, d->mask_slope, da, accumulate_da, 0, s);
   VSRK_LAUNCH_CHECK("conv_fwd_prelu_bwd_final");
   return VSRK_OK;
 }

@@ -131,31 +131,33 @@ __global__ __launch_bounds__(256) void prelu_partial_kernel(View y, View dx, int
   if (threadIdx.x == 0) part[blockIdx.x] = sh[0];
 }
 
-// 1024 lanes, both of a lane's partials loaded before the adds (a 256-lane
-// loop over the 2048 partials was a chain of 8 dependent loads per lane)
-__global__ __launch_bounds__(1024) void prelu_final_kernel(const double* __restrict__ part, int nblk,
-                                                           const float* __restrict__ a, float* __restrict__ da,
-                                                           int accumulate, int pre = 0) {
-  __shared__ double sh[1024];
+// Fixed-order sum of <= a few thousand double partials (one per wave or
+// workgroup): 256 lanes, U independent loads in flight per lane, then a
+// fixed LDS tree.  pre = 0: output-based partials (sum dx y), divided by a^2
+// -- the tape holds PReLU outputs, y < 0 marks x < 0 only while a > 0, so a
+// slope <= 0 poisons da with NaN (the nets route such slopes through pre = 1,
+// the pre-activation form: partials are already sum_{x<0} g x).
+__global__ __launch_bounds__(256) void slope_final_kernel(const double* __restrict__ part, int n,
+                                                          const float* __restrict__ a, float* __restrict__ da,
+                                                          int accumulate, int pre) {
+  constexpr int U = 4;
+  __shared__ double sh[256];
   double s = 0.0;
-  for (int b = threadIdx.x; b < nblk; b += 2048) {
-    const double p0 = part[b];
-    const double p1 = b + 1024 < nblk ? part[b + 1024] : 0.0;
-    s += p0 + p1;
+  for (int base = threadIdx.x; base < n; base += 256 * U) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = base + 256 * u < n ? part[base + 256 * u] : 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += v[u];
   }
   sh[threadIdx.x] = s;
   __syncthreads();
-  for (int k = 512; k > 0; k >>= 1) {
+  for (int k = 128; k > 0; k >>= 1) {
     if (threadIdx.x < k) sh[threadIdx.x] += sh[threadIdx.x + k];
     __syncthreads();
   }
   if (threadIdx.x == 0) {
     const double av = (double)*a;
-    // The tape holds PReLU outputs only: y < 0 marks x < 0 only while a > 0.
-    // A slope <= 0 makes the output-based gradient ambiguous, so it poisons
-    // da with NaN (a loud failure in the optimizer step, never a silently
-    // wrong gradient); nn.PReLU starts at 0.2 (drf_net.py:56).
-    // (pre: the partials are already sum_{x<0} g x, any slope)
     const float v = pre ? (float)sh[0] : av > 0.0 ? (float)(sh[0] / (av * av)) : __builtin_nanf("");
     *da = accumulate ? *da + v : v;
   }
@@ -192,6 +194,11 @@ extern "C" int vsrk_subpixel_wgrad_fold(const float* dweq, const float* dbeq, in
   return VSRK_OK;
 }
 
+void vsrk_slope_final(const double* part, int nparts, const float* a, float* da, int accumulate, int pre,
+                      hipStream_t s) {
+  slope_final_kernel<<<1, 256, 0, s>>>(part, nparts, a, da, accumulate, pre);
+}
+
 extern "C" size_t vsrk_prelu_workspace_size(void) { return PRELU_BLOCKS * sizeof(double); }
 
 extern "C" int vsrk_prelu_wgrad(const vsrk_tensor5* y, const vsrk_tensor5* dx, const float* a, float* da,
@@ -213,7 +220,7 @@ extern "C" int vsrk_prelu_wgrad(const vsrk_tensor5* y, const vsrk_tensor5* dx, c
   else
     prelu_partial_kernel<float><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vd, nvox, part);
   VSRK_LAUNCH_CHECK("prelu_partial");
-  prelu_final_kernel<<<1, 1024, 0, s>>>(part, PRELU_BLOCKS, a, da, accumulate);
+  vsrk_slope_final(part, PRELU_BLOCKS, a, da, accumulate, 0, s);
   VSRK_LAUNCH_CHECK("prelu_final");
   return VSRK_OK;
 }
@@ -231,7 +238,7 @@ namespace {
 // DRF step.
 template <typename T>
 // pre = 0: y is the PReLU OUTPUT (x < 0 read as y < 0, exact while a > 0):
-// slope partials sum dx * y, divided by a^2 in prelu_final_kernel.
+// slope partials sum dx * y, divided by a^2 in vsrk_slope_final.
 // pre = 1: y is the PRE-ACTIVATION x (nn.PReLU's own saved input, any a):
 // dx = x > 0 ? g : a g, slope partials sum_{x<0} g x (g = dy [+ dy2] in fp32)
 __global__ __launch_bounds__(256) void prelu_bwd_kernel(View y, View dy, View dy2, int has2, const float* __restrict__ a,
@@ -377,6 +384,7 @@ static int prelu_bwd_impl(const vsrk_tensor5* y, const vsrk_tensor5* dy, const v
     if (!t) continue;
     if (((uintptr_t)t->ptr) % 16 || t->sn % E || t->sd % E || t->sh % E || t->sw % E) vec = 0;
   }
+  VSRK_CHECK(((uintptr_t)workspace & 15) == 0, "prelu_bwd: workspace must be 16-byte aligned");
   hipStream_t s = (hipStream_t)stream;
   double* part = (double*)workspace;
   if (y->dtype == VSRK_BF16)
@@ -386,7 +394,7 @@ static int prelu_bwd_impl(const vsrk_tensor5* y, const vsrk_tensor5* dy, const v
   else
     prelu_bwd_kernel<float><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, (int)nr64, vec, part, pre);
   VSRK_LAUNCH_CHECK("prelu_bwd");
-  prelu_final_kernel<<<1, 1024, 0, s>>>(part, PRELU_BLOCKS, a, da, accumulate_da, pre);
+  vsrk_slope_final(part, PRELU_BLOCKS, a, da, accumulate_da, pre, s);
   VSRK_LAUNCH_CHECK("prelu_final");
   return VSRK_OK;
 }

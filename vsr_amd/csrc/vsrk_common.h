@@ -119,6 +119,20 @@ __device__ __forceinline__ int64_t view_off(const View& v, int n, int d, int h, 
   return n * v.sn + d * v.sd + (int64_t)(h * v.r + i) * v.sh + (int64_t)(w * v.r + j) * v.sw + cc;
 }
 
+// ---- PReLU slope gradient partials ----
+// The fused and separate PReLU backward kernels (drf.hip, conv_roll.hip,
+// conv_pw.hip) reduce sum_{x<0} g x to one double per wave (or workgroup)
+// in a fixed order; vsrk_slope_final (drf.hip) sums those in a fixed order
+// into *da.  (A last-workgroup finish inside the producing kernel needs an
+// agent-scope release per workgroup -- an L2 writeback on gfx950 -- and made
+// the DRF step 20 % slower; the per-lane float partials of round 4 made the
+// final launch read 64 K floats, 19 us each.)
+__device__ __forceinline__ double vsrk_wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
 // ---- host-side dtype helpers ----
 // 16-bit storage types (bf16, fp16) share every kernel family; the MFMA
 // flavour follows the type (v_mfma_f32_32x32x16_bf16 / _f16).

@@ -45,21 +45,35 @@ struct vsrk_roll_bnred {
   size_t ws_floats;
   int ntiles, ntn;
 };
+// a fused PReLU backward's slope-gradient partials (one double per wave,
+// vsrk_wave_sum) and their capacity; vsrk_slope_final sums them into *da
+struct vsrk_slope_out {
+  double* part;
+  size_t cap;     // doubles
+  int* nparts;    // out: partials written
+};
+void vsrk_slope_final(const double* part, int nparts, const float* a, float* da, int accumulate, int pre,
+                      hipStream_t s);
 int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
-                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s, float* slope_ws = nullptr,
-                       int* slope_blocks = nullptr, vsrk_roll_bnred* bnred = nullptr);
+                       const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s,
+                       const vsrk_slope_out* slope = nullptr, vsrk_roll_bnred* bnred = nullptr);
 // the fused reduce's final per-channel sums (roll_bnred_final_kernel)
 int vsrk_roll_bnred_final(const vsrk_roll_bnred& r, int cout, float* sum_dy, float* sum_dy_xhat, hipStream_t s);
 size_t vsrk_roll_bnred_ws_floats(const vsrk_tensor5* y);
-size_t vsrk_roll_slope_ws_floats();
+size_t vsrk_roll_slope_ws_bytes();
 void vsrk_conv_set_roll_mode(int mode);
+void vsrk_conv_set_roll_wr_mode(int mode);
 
 // pointwise (1x1x1) bf16 conv (conv_pw.hip): forward / data gradient and
 // weight gradient; same return convention (the wgrad launches its own reduce)
 int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
                      const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                      const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
+int vsrk_conv_fwd_pw_pbwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed,
+                          const vsrk_tensor5* mask, const vsrk_tensor5* y, int c_lo, const vsrk_slope_out* slope,
+                          hipStream_t s);
+size_t vsrk_pw_pbwd_ws_bytes();
 size_t vsrk_conv_wgrad_pw_workspace(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk_tensor5* dy);
 int vsrk_conv_wgrad_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk_tensor5* dy,
                        const float* pro_scale, const float* pro_shift, float dy_scale, int32_t perm_r, float* dw,

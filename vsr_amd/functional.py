@@ -220,21 +220,22 @@ def _launched(rc) -> bool:
 
 def conv_prelu_bwd(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, y_fwd: torch.Tensor,
                    a: torch.Tensor, da: torch.Tensor, accumulate_da: bool, *, x_shuffle: int = 1, y_shuffle: int = 1,
-                   subpixel: int = 0) -> bool:
-    """y = conv(x) * (y_fwd > 0 ? 1 : a) and da [+]= the PReLU slope gradient
-    (vsrk_conv_fwd_prelu_bwd): conv followed by prelu_bwd(y_fwd, y, a, y, da)
-    in one kernel.  False when the shape is not eligible (nothing launched)."""
+                   subpixel: int = 0, accumulate: bool = False, c_lo: int = 0) -> bool:
+    """y = (conv(x) [+ y]) * (y_fwd > 0 ? 1 : a) on channels >= c_lo and da
+    [+]= the PReLU slope gradient (vsrk_conv_fwd_prelu_bwd): conv [accumulate]
+    followed by prelu_bwd(y_fwd, y, a, y, da) on y[..., c_lo:] in one kernel.
+    False when the shape is not eligible (nothing launched)."""
     if not FUSE:
         return False
     lib = _lib()
-    d = _desc(k, pad, mask_slope=a, subpixel=subpixel)
+    d = _desc(k, pad, accumulate=accumulate, mask_slope=a, subpixel=subpixel)
     xv, yv, mv = N.t5(x, x_shuffle), N.t5(y, y_shuffle), N.t5(y_fwd, y_shuffle)
     ws = workspace(lib.vsrk_conv_prelu_bwd_workspace(), y.device)
 
     def launch():
         return lib.vsrk_conv_fwd_prelu_bwd(C.byref(d), C.byref(xv), wp.data_ptr(), None, C.byref(mv), C.byref(yv),
-                                           da.data_ptr(), 1 if accumulate_da else 0, ws.data_ptr(), ws.numel(),
-                                           N.stream_ptr(y.device))
+                                           int(c_lo), da.data_ptr(), 1 if accumulate_da else 0, ws.data_ptr(),
+                                           ws.numel(), N.stream_ptr(y.device))
 
     rc = (timer.wrap(("conv_fwd", tuple(k)), xv, yv, launch, _launched) if timer is not None else launch())
     if rc == 2:  # VSRK_ERR_UNSUPPORTED
@@ -340,9 +341,13 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, k, pad, dw: torch.Tensor, dbia
 
 
 def set_conv_path(path: str, mode: int) -> None:
-    """Select a conv kernel family ("fast", "pw", "roll", "thin", "wgrad_pipe", "wgrad_roll", "wgrad_row"): -1 default, 0 off, 1 on
+    """Select a conv kernel family ("fast", "pw", "roll", "roll_wr", "thin", "wgrad_pipe", "wgrad_roll", "wgrad_row"):
+    -1 default, 0 off, 1 on
     (for "roll" / "wgrad_roll": 1 forces the rolling kernel on every eligible
-    shape, the default also skips shallow output depths where it is slower)."""
+    shape, the default also skips shallow output depths where it is slower;
+    "wgrad_row": 2 also takes the sub-pixel tap-skip views; "roll_wr": the
+    rolling conv's resident weights, 2 also with the prefetched residual / mask
+    epilogue, where they are slower)."""
     N.check(_lib().vsrk_conv_set_path(path.encode(), int(mode)), "conv_set_path")
 
 
@@ -682,8 +687,7 @@ def prelu_bwd(y: torch.Tensor, dy: torch.Tensor, a: torch.Tensor, dx: torch.Tens
     pre-activation x (vsrk_prelu_bwd_pre, any slope): dx = g (x > 0 ? 1 : a),
     da [+]= sum_{x<0} g x with g = dy [+ dy2]."""
     lib = _lib()
-    nb = lib.vsrk_prelu_workspace_size()
-    ws = workspace(nb, y.device)
+    ws = workspace(lib.vsrk_prelu_workspace_size(), y.device)
     yv, gv, ov = N.t5(y), N.t5(dy), N.t5(dx)
     g2 = N.t5(dy2) if dy2 is not None else None
     fn = lib.vsrk_prelu_bwd_pre if pre else lib.vsrk_prelu_bwd

@@ -153,6 +153,9 @@ class _DRFBase(BaseNet):
     _OVERLAP_WGRAD = True  # per-frame launches leave CUs idle: weight gradients fill them
     # weight gradients batched over the sequence (see the module docstring)
     SEQ_WGRAD = os.environ.get("VSR_DRF_SEQ_WGRAD", "1") != "0"
+    # the PReLU backwards over concat-gradient slices fused into their last
+    # producer (round 5; VSR_DRF_FUSE_SLICES=0 for A/B)
+    FUSE_SLICES = os.environ.get("VSR_DRF_FUSE_SLICES", "1") != "0"
     def __init__(self, in_channels, out_channels, num_features, num_groups, upscale_factor):
         super().__init__()
         self.in_channels = in_channels
@@ -360,8 +363,8 @@ class _DRFBase(BaseNet):
             for _, st_ in reversed(self._ups()):
                 hh0, ww0 = hh0 // st_, ww0 // st_
                 fe += hh0 * ww0 * f  # dup{j}
-            fe += (2 * G + 2) * h * w * f + h * w * 4 * f  # gout, gl*, dt1_*, g0, gin, du_u1
-            fe += (2 * G - 1) * H * W * f  # gh*, dt2_*
+            fe += (2 * G + 2) * h * w * f + h * w * 4 * f  # gout, dL ((G + 1) f), dt1_*, gin, du_u1
+            fe += (2 * G - 1) * H * W * f  # dHc (G f), dt2_*
             frame_bytes = fe * b * torch.empty((), dtype=cd).element_size()
             budget = float(os.environ.get("VSR_DRF_SEQ_BUDGET_GB", "16")) * 2 ** 30
             Kg = max(1, min(T, int(budget // max(frame_bytes, 1))))
@@ -462,6 +465,20 @@ class _DRFBase(BaseNet):
 
             defer(conv.weight, t, x, dy, run, acc)
 
+        def fuse(pr, call) -> bool:
+            """the PReLU pr's backward fused into its gradient's last producer:
+            call(da, accumulate_da) -> launched (F.conv_prelu_bwd); never for a
+            slope <= 0 (the fused epilogues read the PReLU output)"""
+            if id(pr) in nonpos or not self.FUSE_SLICES:
+                return False
+            existed = id(pr.weight) in bufs
+            da, acc = gbuf(pr.weight)
+            if call(da, acc):
+                return True
+            if not existed:  # nothing written: the unfused backward starts da
+                del bufs[id(pr.weight)]
+            return False
+
         def prelu(y, dy, pr, out, dy2=None, pre=None):
             """PReLU backward from its output y; for a slope <= 0 from the
             pre-activation that pre() recomputes from the tape (the producing
@@ -504,25 +521,49 @@ class _DRFBase(BaseNet):
             # out_block's data gradient; dHc (every slice) by the last group's
             # 1x1 down-projection gradient (group 0's strided conv when G = 1);
             # dL[..., :f] has mixed first contributors and is zeroed.
-            dL = new(h, w, (G + 1) * f)
+            # The concat gradients are sequence buffers too: each PReLU
+            # backward over a slice runs in place, fused into the slice's last
+            # producer where it can (the slice is the producer's tail channels,
+            # c_lo), and the weight gradients read the slices.
+            dL = sbuf("dL", t, h, w, (G + 1) * f)
             dL[..., :f].zero_()
-            dHc = new(H, W, G * f)
-            F.conv(gout, pw(fb.out_block.conv, 1), dL[..., f:], K1, P0)
+            dHc = sbuf("dHc", t, H, W, G * f)
+            done = set()  # slices whose PReLU backward ran fused: ("l", i) / ("h", i) / "g0"
+
+            def dnpr(i_):  # the PReLU after down projection i_ (lr_{i_+1})
+                return fb.down_blocks[i_].prelu if i_ == 0 else fb.down_blocks[i_].prelu2
+
+            def uppr(i_):  # the PReLU after up projection i_ (hr_{i_})
+                return fb.up_blocks[i_].prelu if i_ == 0 else fb.up_blocks[i_].prelu2
+
+            wo = pw(fb.out_block.conv, 1)
+            if fuse(dnpr(G - 1), lambda da, acc: F.conv_prelu_bwd(
+                    gout, wo, dL[..., f:], K1, P0, L[..., f:], dnpr(G - 1).weight, da, acc, c_lo=(G - 1) * f)):
+                done.add(("l", G - 1))
+            else:
+                F.conv(gout, wo, dL[..., f:], K1, P0)
             for i in range(G - 1, -1, -1):
                 up, dn = fb.up_blocks[i], fb.down_blocks[i]
                 # down projection -> lr_{i+1} = L[..., (i+1)f:(i+2)f]
                 cv, cpr = (dn.conv, dn.prelu) if i == 0 else (dn.conv2, dn.prelu2)
                 sl = slice((i + 1) * f, (i + 2) * f)
                 hsrc = Hc[..., :f] if i == 0 else rc["t2s"][i]
-                gl = prelu(L[..., sl], dL[..., sl], cpr, sbuf(f"gl{i}", t, h, w, f),
-                           pre=lambda cv=cv, hsrc=hsrc: F.conv(
-                               hsrc, sp(cv, False)[0], new(h, w, f), K3, P1, bias=sp(cv, False)[1], x_shuffle=s,
-                               subpixel=F.subpixel_code(k, s, p, False, False)))
+                gl = dL[..., sl]
+                if ("l", i) not in done:
+                    prelu(L[..., sl], gl, cpr, gl,
+                          pre=lambda cv=cv, hsrc=hsrc: F.conv(
+                              hsrc, sp(cv, False)[0], new(h, w, f), K3, P1, bias=sp(cv, False)[1], x_shuffle=s,
+                              subpixel=F.subpixel_code(k, s, p, False, False)))
                 sp_wgrad(cv, hsrc, gl, False, t)
                 wq1, _ = sp(cv, False, 1)
                 spc = F.subpixel_code(k, s, p, False, True)
                 if i == 0:
-                    F.conv(gl, wq1, dHc[..., :f], K3, P1, y_shuffle=s, accumulate=G > 1, subpixel=spc)
+                    if fuse(uppr(0), lambda da, acc: F.conv_prelu_bwd(
+                            gl, wq1, dHc[..., :f], K3, P1, Hc[..., :f], uppr(0).weight, da, acc, y_shuffle=s,
+                            subpixel=spc, accumulate=G > 1)):
+                        done.add(("h", 0))
+                    else:
+                        F.conv(gl, wq1, dHc[..., :f], K3, P1, y_shuffle=s, accumulate=G > 1, subpixel=spc)
                 else:
                     dt2 = sbuf(f"dt2_{i}", t, H, W, f)
                     da, acc = gbuf(dn.prelu1.weight)
@@ -535,20 +576,34 @@ class _DRFBase(BaseNet):
                         F.conv(gl, wq1, dt2, K3, P1, y_shuffle=s, subpixel=spc)
                         F.prelu_bwd(rc["t2s"][i], dt2, dn.prelu1.weight, dt2, da, acc)
                     wgrad(dn.conv1, Hc[..., :(i + 1) * f], dt2, K1, P0, t)
-                    F.conv(dt2, pw(dn.conv1, 1), dHc[..., :(i + 1) * f], K1, P0, accumulate=i != G - 1)
+                    wd1 = pw(dn.conv1, 1)
+                    if fuse(uppr(i), lambda da, acc: F.conv_prelu_bwd(
+                            dt2, wd1, dHc[..., :(i + 1) * f], K1, P0, Hc[..., :(i + 1) * f], uppr(i).weight, da, acc,
+                            accumulate=i != G - 1, c_lo=i * f)):
+                        done.add(("h", i))
+                    else:
+                        F.conv(dt2, wd1, dHc[..., :(i + 1) * f], K1, P0, accumulate=i != G - 1)
                 # up projection -> hr_i = Hc[..., i f:(i+1) f]
                 dec, dpr = (up.deconv, up.prelu) if i == 0 else (up.deconv2, up.prelu2)
                 sh = slice(i * f, (i + 1) * f)
                 src = L[..., :f] if i == 0 else rc["t1s"][i]
-                gh = prelu(Hc[..., sh], dHc[..., sh], dpr, sbuf(f"gh{i}", t, H, W, f),
-                           pre=lambda dec=dec, src=src: F.conv(
-                               src, sp(dec, True)[0], new(H, W, f), K3, P1, bias=sp(dec, True)[1], bias_r=1,
-                               y_shuffle=s, subpixel=F.subpixel_code(k, s, p, True, False)))
+                gh = dHc[..., sh]
+                if ("h", i) not in done:
+                    prelu(Hc[..., sh], gh, dpr, gh,
+                          pre=lambda dec=dec, src=src: F.conv(
+                              src, sp(dec, True)[0], new(H, W, f), K3, P1, bias=sp(dec, True)[1], bias_r=1,
+                              y_shuffle=s, subpixel=F.subpixel_code(k, s, p, True, False)))
                 sp_wgrad(dec, src, gh, True, t)
                 wq1, _ = sp(dec, True, 1)
                 spc = F.subpixel_code(k, s, p, True, True)
                 if i == 0:
-                    F.conv(gh, wq1, dL[..., :f], K3, P1, x_shuffle=s, accumulate=True, subpixel=spc)
+                    ipr = fb.in_block.prelu
+                    if fuse(ipr, lambda da, acc: F.conv_prelu_bwd(
+                            gh, wq1, dL[..., :f], K3, P1, L[..., :f], ipr.weight, da, acc, x_shuffle=s,
+                            subpixel=spc, accumulate=True)):
+                        done.add("g0")
+                    else:
+                        F.conv(gh, wq1, dL[..., :f], K3, P1, x_shuffle=s, accumulate=True, subpixel=spc)
                 else:
                     dt1 = sbuf(f"dt1_{i}", t, h, w, f)
                     da, acc = gbuf(up.prelu1.weight)
@@ -561,9 +616,18 @@ class _DRFBase(BaseNet):
                         F.conv(gh, wq1, dt1, K3, P1, x_shuffle=s, subpixel=spc)
                         F.prelu_bwd(rc["t1s"][i], dt1, up.prelu1.weight, dt1, da, acc)
                     wgrad(up.conv1, L[..., :(i + 1) * f], dt1, K1, P0, t)
-                    F.conv(dt1, pw(up.conv1, 1), dL[..., :(i + 1) * f], K1, P0, accumulate=True)
-            g0 = prelu(L[..., :f], dL[..., :f], fb.in_block.prelu, sbuf("g0", t, h, w, f),
-                       pre=lambda: F.conv(X0, pw(fb.in_block.conv), new(h, w, f), K1, P0, bias=fb.in_block.conv.bias))
+                    wu1 = pw(up.conv1, 1)
+                    # the last contribution to lr_i's gradient (slice i of dL)
+                    if fuse(dnpr(i - 1), lambda da, acc: F.conv_prelu_bwd(
+                            dt1, wu1, dL[..., :(i + 1) * f], K1, P0, L[..., :(i + 1) * f], dnpr(i - 1).weight, da,
+                            acc, accumulate=True, c_lo=i * f)):
+                        done.add(("l", i - 1))
+                    else:
+                        F.conv(dt1, wu1, dL[..., :(i + 1) * f], K1, P0, accumulate=True)
+            g0 = dL[..., :f]
+            if "g0" not in done:
+                prelu(L[..., :f], g0, fb.in_block.prelu, g0,
+                      pre=lambda: F.conv(X0, pw(fb.in_block.conv), new(h, w, f), K1, P0, bias=fb.in_block.conv.bias))
             wgrad(fb.in_block.conv, X0, g0, K1, P0, t)
             dX0 = F.conv(g0, pw(fb.in_block.conv, 1), new(h, w, 2 * f), K1, P0)
             if t == 0:  # the first hidden state is in_features itself
@@ -574,9 +638,13 @@ class _DRFBase(BaseNet):
             gin = prelu(X0[..., :f], gfeat, ib.prelu2, sbuf("gin", t, h, w, f), dy2=dX0[..., :f],
                         pre=lambda: F.conv(rc["u1"], pw(ib.conv2), new(h, w, f), K1, P0, bias=ib.conv2.bias))
             wgrad(ib.conv2, rc["u1"], gin, K1, P0, t)
-            du1 = F.conv(gin, pw(ib.conv2, 1), sbuf("du_u1", t, h, w, 4 * f), K1, P0)
-            prelu(rc["u1"], du1, ib.prelu1, du1,
-                  pre=lambda: F.conv(rc["xv"], pw(ib.conv1), new(h, w, 4 * f), K3, P1, bias=ib.conv1.bias))
+            du1 = sbuf("du_u1", t, h, w, 4 * f)
+            wi2 = pw(ib.conv2, 1)
+            if not fuse(ib.prelu1, lambda da, acc: F.conv_prelu_bwd(gin, wi2, du1, K1, P0, rc["u1"], ib.prelu1.weight,
+                                                                      da, acc)):
+                F.conv(gin, wi2, du1, K1, P0)
+                prelu(rc["u1"], du1, ib.prelu1, du1,
+                      pre=lambda: F.conv(rc["xv"], pw(ib.conv1), new(h, w, 4 * f), K3, P1, bias=ib.conv1.bias))
             wgrad(ib.conv1, rc["xv"], du1, K3, P1, t)
             launch_runs(t)
         for prm, g in bufs.values():
