@@ -552,6 +552,26 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
   const bool f_mask = EIN == 1 ? a.has_mask != 0 : false;
   const bool f_acc = EIN == 1 ? a.accumulate != 0 : (EIN == EIN_ACC || EIN == EIN_PBACC);
   const bool f_pb = EIN == 1 ? a.pbwd != 0 : (EIN == EIN_PB || EIN == EIN_PBACC);
+  // Store-pass chunk k of a lane: row-major (2 rows of every column per k),
+  // or, in the compile-time forms with whole 64-channel column groups, 8 rows
+  // x one 64-channel group per k -- so "is this chunk on the PReLU tail" is
+  // the same for the whole wave and the tail work is a scalar branch
+  constexpr int OCPR_ = COP / 8;
+  constexpr bool BLK = EIN >= 2 && OCPR_ % 8 == 0;
+  constexpr int NGRP = OCPR_ / 8;
+  auto chunk_rc = [&](int ln, int k, int& row, int& c) __attribute__((always_inline)) {
+    if constexpr (BLK) {
+      row = 8 * (k / NGRP) + (ln >> 3);
+      c = 8 * (8 * (k % NGRP) + (ln & 7));
+    } else {
+      const int i = ln + 64 * k;
+      row = i / OCPR_;
+      c = 8 * (i % OCPR_);
+    }
+  };
+  auto on_tail = [&](int k, int c) __attribute__((always_inline)) {  // BLK: wave-uniform
+    return BLK ? co0 + 64 * (k % NGRP) >= a.pm_lo : co0 + c >= a.pm_lo;
+  };
   auto ein_load = [&](int tile, uint4 (&em)[EIN ? EIN_NOK : 1], uint4 (&ey)[EIN ? EIN_NOK : 1])
                       __attribute__((always_inline)) {
     if constexpr (EIN) {
@@ -564,13 +584,18 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
       const Rsrc rm = rsrc_at(reinterpret_cast<const H*>(a.msk ? a.msk : a.y) + (int64_t)tb.n0 * a.msn);
 #pragma unroll
       for (int k = 0; k < EIN_NOK; ++k) {
-        const int i = ln + 64 * k, row = i / OCPR, c = 8 * (i % OCPR);
+        int row, c;
+        chunk_rc(ln, k, row, c);
         const bool ok = co0 + c < a.cout;
         if (EIN == 1) {
           if (f_mask || (f_pb && co0 + c >= a.pm_lo))
             em[k] = bload16(rm, ok ? row_off(tb, row, v0, a.msn, a.msw) + 2 * (co0 + c) : PW_OOB);
-        } else if (f_pb) {  // branch-free: chunks below pm_lo read nothing (out-of-range offset) and see m = 0
-          em[k] = bload16(rm, ok && co0 + c >= a.pm_lo ? row_off(tb, row, v0, a.msn, a.msw) + 2 * (co0 + c) : PW_OOB);
+        } else if (f_pb) {
+          if (BLK) {
+            if (on_tail(k, c)) em[k] = bload16(rm, ok ? row_off(tb, row, v0, a.msn, a.msw) + 2 * (co0 + c) : PW_OOB);
+          } else {  // branch-free: chunks below pm_lo read nothing (out-of-range offset) and see m = 0
+            em[k] = bload16(rm, ok && on_tail(k, c) ? row_off(tb, row, v0, a.msn, a.msw) + 2 * (co0 + c) : PW_OOB);
+          }
         }
         if (f_acc) ey[k] = bload16(ry, ok ? row_off(tb, row, v0, a.ysn, a.ysw) + 2 * (co0 + c) : PW_OOB);
       }
@@ -732,7 +757,8 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
       const float mslope = (EIN && a.mask_slope) ? *a.mask_slope : 0.f;
 #pragma unroll
       for (int k = 0; k < NOK; ++k) {
-        const int i = ln + 64 * k, row = i / OCPR, c = 8 * (i % OCPR);
+        int row, c;
+        chunk_rc(ln, k, row, c);
         uint4 v = *reinterpret_cast<const uint4*>(buf + row * RS + c * 2);
         if constexpr (EIN) {
           float o[8];
@@ -750,8 +776,8 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_fwd_staged_kernel(PwArgs a) {
             for (int e = 0; e < 8; ++e) o[e] += yo[e];
           }
           v = Chunk<H>::pack(o);
-          if (EIN != 1 && f_pb) {
-            const bool tail = co0 + c >= a.pm_lo;
+          if (EIN != 1 && f_pb && (!BLK || on_tail(k, c))) {
+            const bool tail = BLK || on_tail(k, c);
             float m[8], tr[8];
             Chunk<H>::unpack(em[k], m);
 #pragma unroll

@@ -1364,14 +1364,14 @@ extern "C" int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* d, const vsrk_tenso
                                        const float* bias, const vsrk_tensor5* y_fwd, const vsrk_tensor5* y,
                                        int32_t c_lo, float* da, int32_t accumulate_da, void* workspace,
                                        size_t workspace_bytes, void* stream) {
-  VSRK_CHECK(d && x && y && y_fwd && w_packed && da && d->mask_slope, "conv_fwd_prelu_bwd: null argument");
+  VSRK_CHECK(d && x && y && y_fwd && w_packed && d->mask_slope, "conv_fwd_prelu_bwd: null argument");
   VSRK_CHECK(workspace && workspace_bytes >= vsrk_conv_prelu_bwd_workspace(),
              "conv_fwd_prelu_bwd: workspace %zu < %zu bytes", workspace_bytes, vsrk_conv_prelu_bwd_workspace());
   VSRK_CHECK(((uintptr_t)workspace & 15) == 0, "conv_fwd_prelu_bwd: workspace must be 16-byte aligned");
   VSRK_CHECK(c_lo >= 0 && c_lo < y->c, "conv_fwd_prelu_bwd: c_lo %d outside [0, %d)", c_lo, y->c);
   hipStream_t s = (hipStream_t)stream;
   if ((int64_t)y->n * y->d * y->h * y->w == 0) {  // nothing to launch: no slope gradient
-    if (!accumulate_da) (void)hipMemsetAsync(da, 0, sizeof(float), s);
+    if (da && !accumulate_da) (void)hipMemsetAsync(da, 0, sizeof(float), s);
     return VSRK_OK;
   }
   int nparts = 0;
@@ -1387,8 +1387,10 @@ extern "C" int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* d, const vsrk_tenso
   }
   if (rc == 0) return VSRK_ERR_UNSUPPORTED;
   if (rc < 0) return -rc;
-  vsrk_slope_final((const double*)workspace, nparts, d->mask_slope, da, accumulate_da, 0, s);
-  VSRK_LAUNCH_CHECK("conv_fwd_prelu_bwd_final");
+  if (da) {  // (da == NULL: the partials stay in the workspace slot, vsrk_slope_final_sum later)
+    vsrk_slope_final((const double*)workspace, nparts, d->mask_slope, da, accumulate_da, 0, s);
+    VSRK_LAUNCH_CHECK("conv_fwd_prelu_bwd_final");
+  }
   return VSRK_OK;
 }
 
