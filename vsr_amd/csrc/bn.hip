@@ -307,6 +307,9 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(View x, View dz,
   }
 }
 
+#ifndef BN_MULTI_U  // voxels per pass (A/B knob; r5 same-box DUF step: U = 4 +0.6 ms, U = 1 flat)
+#define BN_MULTI_U 2
+#endif
 // NC contributors' BN+ReLU backward applies into one output block (see
 // vsrk_bn_relu_bwd_apply_multi): the same row walk and per-thread constants
 // as bn_relu_bwd_apply_kernel, x and dx moved once, each contributor's dz
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_multi_kernel(View x, Vi
     }
     // U voxels per pass with every load (x, dx, each active dz) issued before
     // any is used; a scalar path for a partial last chunk
-    constexpr int U = 2;
+    constexpr int U = BN_MULTI_U;
     for (int wb = vl; wb < x.w; wb += U * vpb) {
       uint4 rx[U], ro[U], rg[NC][U];
 #pragma unroll
