@@ -342,6 +342,12 @@ int vsrk_conv_fwd_stencil(const vsrk_conv_desc* d, const vsrk_tensor5* x, const 
   }
   const int want = (int)vsrk_capped_grid((int64_t)st_num_cus() * per_cu);
   a.tiles_per_blk = (int)ceil_div64(ntiles, want);
+  // small launches (DRF's 1 -> 64 data gradient at 4 x 512^2: 2048 tiles) at
+  // one tile per workgroup spend it on the per-workgroup setup (each lane's
+  // 72 weights, the first patch): at least 4 tiles while the grid still
+  // covers every CU
+  if (vsrk_g_grid_cap <= 0)
+    a.tiles_per_blk = std::max(a.tiles_per_blk, (int)std::min<int64_t>(4, std::max<int64_t>(1, ntiles / st_num_cus())));
   const int grid = (int)ceil_div64(ntiles, a.tiles_per_blk);
   vsrk_dispatch16(x->dtype, [&](auto tag) {
     using H = decltype(tag);

@@ -261,11 +261,24 @@ class _DRFBase(BaseNet):
             XV = F.to_view(torch.cat([x.float() for x in frames]), cd, cpad=8)[..., :cin]  # (T*b, 1, h, w, cin)
         outs, recs = [], []
         X0 = buf("X0", 0, h, w, 2 * f, T + 1)
+        batched = seqs is not None
+        if batched:
+            # in_features = in_block(x_t) does not depend on the recurrence
+            # (drf_net.py:40-41): both in_block convs run once over all T
+            # frames (per frame they were 2 x 30 launches of a few hundred
+            # 8 x 32 tiles each, latency-bound: the 1 -> 4F conv at 77 us)
+            buf("u1", 0, h, w, 4 * f)  # creates the (T, B, h, w, 4F) sequence buffer
+            U1 = seqs["u1"].view(T * b, 1, h, w, 4 * f)
+            F.conv(XV, pw(ib.conv1), U1, K3, P1, bias=ib.conv1.bias, act=PR, act_param=ib.prelu1.weight)
+            X0s = seqs["X0"][:T].view(T * b, 1, h, w, 2 * f)
+            F.conv(U1, pw(ib.conv2), X0s[..., :f], K1, P0, bias=ib.conv2.bias, act=PR, act_param=ib.prelu2.weight)
         for t, x in enumerate(frames):
             xv = XV[t * b:(t + 1) * b] if XV is not None else F.to_view(x, cd, cpad=8)[..., :cin]
             u1 = buf("u1", t, h, w, 4 * f)
-            F.conv(xv, pw(ib.conv1), u1, K3, P1, bias=ib.conv1.bias, act=PR, act_param=ib.prelu1.weight)
-            F.conv(u1, pw(ib.conv2), X0[..., :f], K1, P0, bias=ib.conv2.bias, act=PR, act_param=ib.prelu2.weight)
+            if not batched:
+                F.conv(xv, pw(ib.conv1), u1, K3, P1, bias=ib.conv1.bias, act=PR, act_param=ib.prelu1.weight)
+                F.conv(u1, pw(ib.conv2), X0[..., :f], K1, P0, bias=ib.conv2.bias, act=PR,
+                       act_param=ib.prelu2.weight)
             if t == 0:  # hidden_state = in_features (drf_net.py:42-43)
                 F.conv(u1, pw(ib.conv2), X0[..., f:], K1, P0, bias=ib.conv2.bias, act=PR,
                        act_param=ib.prelu2.weight)
