@@ -40,6 +40,11 @@ def _setup(cls, kw, x_shape, y_shape, seq):
      (2, 1, 16, 24), (2, 1, 64, 96), 0),
     ("DRFNet", dict(in_channels=1, out_channels=1, num_features=32, num_groups=2, upscale_factor=4),
      (2, 1, 12, 16), (2, 1, 48, 64), 3),
+    # f = 64: the fused PReLU backwards (rolling / pointwise epilogues) and the
+    # sequence weight-gradient runs under capture -- the form the cfg 3 bench
+    # line replays
+    ("DRFNet", dict(in_channels=1, out_channels=1, num_features=64, num_groups=3, upscale_factor=4),
+     (2, 1, 12, 16), (2, 1, 48, 64), 3),
 ])
 def test_captured_train_step_equals_eager(cls, kw, xs, ys, seq):
     ref_net, ref_step = _setup(cls, kw, xs, ys, seq)
