@@ -75,11 +75,10 @@ DATASET = "acdc"  # synthetic-data normalisation: "acdc", "dsb15" or "mixed" (ha
 CONFIGS = {
     "cfg2": dict(B=4, T=16, dataset="acdc", precision="bf16", models="edsr,duf",
                  desc="ACDC 4x SR, 3D 16x128x128 volumes bf16, batch 4 per GPU"),
-    # cfg3: DRF's recurrent step is ~2000 small launches, ~9 ms of it on the
-    # host: on one GPU the whole step (fwd, loss, bwd, Adam) is replayed from
-    # one HIP graph by default (bitwise equal to the eager step:
-    # tests/test_graph_gpu.py; --no-graph times it eager)
-    "cfg3": dict(B=4, T=30, dataset="dsb15", precision="bf16", models="drf", graph=True,
+    # cfg3: DRF's recurrent step is ~2000 small launches (~9 ms of it host
+    # side); --graph replays the whole step from one HIP graph (DESIGN.md
+    # section 7); eager is the default
+    "cfg3": dict(B=4, T=30, dataset="dsb15", precision="bf16", models="drf",
                  desc="DSB15 cine 4x SR, T=30 2D+t stacks (DRF), batch 4 per GPU"),
     "cfg4": dict(B=2, T=30, H=64, W=64, dataset="acdc", precision="bf16", models="duf",
                  desc="ACDC 4x SR, full 3D cine volumes (2 x 30 frames of 64x64 LR, 256x256 HR, no crop) per GPU"),

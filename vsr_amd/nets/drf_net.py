@@ -368,6 +368,14 @@ class _DRFBase(BaseNet):
             frame_bytes = fe * b * torch.empty((), dtype=cd).element_size()
             budget = float(os.environ.get("VSR_DRF_SEQ_BUDGET_GB", "16")) * 2 ** 30
             Kg = max(1, min(T, int(budget // max(frame_bytes, 1))))
+            if torch.cuda.is_current_stream_capturing():
+                # under HIP-graph capture no chunk is freed mid-backward: a
+                # block freed during capture can go to a later captured
+                # allocation while the side stream's weight-gradient runs
+                # still read it (record_stream does not defer it there) --
+                # the captured cfg 3 step diverged from the eager one
+                # (tools/diag/graph_drf_cfg3.py); the graph pool holds all T
+                Kg = T
         self._seq_run_frames = Kg  # (tests / bench records)
 
         def sbuf(name, t, hh, ww, c):
