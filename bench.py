@@ -75,9 +75,8 @@ DATASET = "acdc"  # synthetic-data normalisation: "acdc", "dsb15" or "mixed" (ha
 CONFIGS = {
     "cfg2": dict(B=4, T=16, dataset="acdc", precision="bf16", models="edsr,duf",
                  desc="ACDC 4x SR, 3D 16x128x128 volumes bf16, batch 4 per GPU"),
-    # cfg3: DRF's recurrent step is ~2000 small launches (~9 ms of it host
-    # side); --graph replays the whole step from one HIP graph (DESIGN.md
-    # section 7); eager is the default
+    # cfg3: DRF's recurrent step (eager; a HIP-graph replay measured slower,
+    # DESIGN.md section 7)
     "cfg3": dict(B=4, T=30, dataset="dsb15", precision="bf16", models="drf",
                  desc="DSB15 cine 4x SR, T=30 2D+t stacks (DRF), batch 4 per GPU"),
     "cfg4": dict(B=2, T=30, H=64, W=64, dataset="acdc", precision="bf16", models="duf",
@@ -292,8 +291,7 @@ def run_model(name, args, world, rank, dev):
     spec = MODELS[name]
     torch.manual_seed(0)  # identical initial weights on every rank
     net = getattr(nets, spec["cls"])(**spec["kwargs"]).to(dev).set_precision(args.precision).train()
-    graph = args.graph and world == 1  # (collectives stay outside graphs)
-    opt = torch.optim.Adam(net.parameters(), lr=1e-4, capturable=graph)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4)
     sync = None
     if world > 1:
         sync = GradSync(net, world)
@@ -323,45 +321,21 @@ def run_model(name, args, world, rank, dev):
         loss.backward()
         if sync is not None:
             sync.finish()
-        if graph or net.step_ok():  # fp16: skip a step whose gradients overflowed (eager only)
+        if net.step_ok():  # fp16: skip a step whose gradients overflowed
             opt.step()
         return loss
 
     match, kdesc = dominant(name, args.precision)
-    if graph:
-        # --graph: the whole step (forward, loss, backward, Adam) captured into
-        # one HIP graph after eager warm-up on a side stream; the timed steps
-        # are replays.  The roofline kernels are timed on one eager step.
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(max(2, args.warmup)):
-                step()
-        torch.cuda.current_stream().wait_stream(side)
-        F.timer = F.KernelTimer(match)
+    for _ in range(args.warmup):
         step()
-        timer, F.timer = F.timer, None
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            loss = step()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            g.replay()
-        torch.cuda.synchronize()
-        F.timer = timer
-        timer.steps = 1
-    else:
-        for _ in range(args.warmup):
-            step()
-        F.timer = F.KernelTimer(match)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            loss = step()
-        torch.cuda.synchronize()
+    F.timer = F.KernelTimer(match)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -397,10 +371,13 @@ def run_model(name, args, world, rank, dev):
                      "kernel_ms_per_step": kernel_s / tsteps * 1e3, "launches_per_step": launches / tsteps,
                      "flop_per_step": flop / tsteps, "by_direction": by_dir},
         "final_loss": float(loss.item()),
-        "graph": graph,
     }
     if comm is not None:
         res["comm"] = comm
+    if getattr(net, "_seq_run_k", None):  # DRF: frames per sequence-buffer chunk and per weight-gradient run
+        ks = net._seq_run_k
+        res["wgrad_runs"] = {"chunk_frames": net._seq_run_frames,
+                             "run_frames": {str(k): sorted(n for n, v in ks.items() if v == k) for k in sorted(set(ks.values()))}}
     res["metrics"] = metrics
     del net, opt, sync
     torch.cuda.empty_cache()
@@ -495,12 +472,8 @@ def main():
     ap.add_argument("--precision", default=None, choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured MFMA / HBM peak microbenchmarks")
-    ap.add_argument("--graph", action="store_true",
-                    help="time replays of the whole step captured into one HIP graph (N = 1)")
-    ap.add_argument("--no-graph", action="store_true", help="eager steps even where the config defaults to a graph")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
-    args.graph = (args.graph or cfg.get("graph", False)) and not args.no_graph
     args.models = args.model or args.models or cfg["models"]
     args.precision = args.precision or cfg["precision"]
     apply_config(args)

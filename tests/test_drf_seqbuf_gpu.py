@@ -17,7 +17,8 @@ pytestmark = pytest.mark.gpu
 T = 6
 
 
-def _grads(monkeypatch, budget_gb=None, seq=True):
+def _grads(monkeypatch, budget_gb=None, seq=True, run_cap=0, with_k=False):
+    monkeypatch.setenv("VSR_DRF_RUN_FRAMES", str(run_cap))
     if budget_gb is not None:
         monkeypatch.setenv("VSR_DRF_SEQ_BUDGET_GB", str(budget_gb))
     else:
@@ -37,8 +38,9 @@ def _grads(monkeypatch, budget_gb=None, seq=True):
     torch.stack([l1(o, t) for o, t in zip(out, y)]).mean().backward()
     torch.cuda.synchronize()
     peak = torch.cuda.max_memory_allocated() - base
-    return ({k: p.grad.detach().clone() for k, p in net.named_parameters()},
-            getattr(net, "_seq_run_frames", None), peak)
+    res = ({k: p.grad.detach().clone() for k, p in net.named_parameters()},
+           getattr(net, "_seq_run_frames", None), peak)
+    return (*res, dict(getattr(net, "_seq_run_k", {}))) if with_k else res
 
 
 def test_chunked_sequence_buffers(monkeypatch):
@@ -59,6 +61,20 @@ def test_chunked_sequence_buffers(monkeypatch):
     gw3, _, _ = _grads(monkeypatch, seq=False)
     for k, v in gw.items():
         err = (gw3[k] - v).norm() / v.norm().clamp_min(1e-30)
+        assert err < 2e-5, (k, float(err))
+
+
+def test_runs_need_not_divide_chunks(monkeypatch):
+    """a run length that does not divide the chunk (Kg = 5 of
+    T = 6, runs of 2 frames: [0,2) [2,4) [4,5) | [5,6)) -- round 5 lowered K
+    until it divided Kg, down to single frames for a prime Kg"""
+    gw, _, _ = _grads(monkeypatch)
+    budget = 5.5 * _frame_bytes() / 2 ** 30
+    gw2, kg, _, run_k = _grads(monkeypatch, budget, run_cap=2, with_k=True)
+    assert kg == 5
+    assert run_k and set(run_k.values()) == {2}, run_k
+    for k, v in gw.items():
+        err = (gw2[k] - v).norm() / v.norm().clamp_min(1e-30)
         assert err < 2e-5, (k, float(err))
 
 

@@ -2,7 +2,10 @@
 synchronises): a whole train step -- forward, L1 loss, hand-written backward,
 Adam -- captured into one HIP graph and replayed gives the same parameters as
 the same steps run eagerly.  EDSR (single stream) and DRF (weight gradients on
-a side stream, joined inside the graph)."""
+a side stream, joined inside the graph).  Captured, DRF cannot read its PReLU
+slopes on the host, so every PReLU backward takes the pre-activation form
+(correct for any slope); the eager reference is put on the same forms, and a
+PReLU with a negative slope is included."""
 import pytest
 import torch
 
@@ -15,6 +18,9 @@ pytestmark = pytest.mark.gpu
 def _setup(cls, kw, x_shape, y_shape, seq):
     torch.manual_seed(0)
     net = getattr(nets, cls)(**kw).cuda().set_precision("bf16").train()
+    if cls == "DRFNet":
+        net.f_block.up_blocks[0].prelu.weight.data.fill_(-0.1)  # a slope <= 0 (nn.PReLU allows any)
+        net._slopes_async = lambda: None  # the captured step's forms, eagerly too
     opt = torch.optim.Adam(net.parameters(), lr=1e-3, capturable=True)
     g = torch.Generator().manual_seed(1)
     if seq:
@@ -64,4 +70,5 @@ def test_captured_train_step_equals_eager(cls, kw, xs, ys, seq):
         ref_step()
     torch.cuda.synchronize()
     for (k, p), (_, q) in zip(net.named_parameters(), ref_net.named_parameters()):
+        assert torch.isfinite(p).all(), k
         assert torch.equal(p.detach(), q.detach()), k

@@ -1178,7 +1178,13 @@ static bool launch_fwd_staged(const PwArgs& a, int grid, int nchunk, bool pro, h
     kern = al ? pw_fwd_staged_kernel<NCB, NKB, M, false, true, 0, EIN_GEN, H>
               : pw_fwd_staged_kernel<NCB, NKB, M, false, false, 0, EIN_GEN, H>;
     if constexpr (NKB == 2) {  // DRF's 64-input-channel data gradients: the branch-free forms
-      if (!a.has_mask && (a.accumulate || a.pbwd)) {
+      // (with whole 64-channel store groups (COP % 64 == 0) the PReLU tail is
+      // decided per group, so it must start on a group boundary; any other
+      // c_lo -- e.g. num_features 48: c_lo = 144 of 192 -- takes the generic
+      // per-chunk form)
+      constexpr bool GROUPED = (COP / 8) % 8 == 0;
+      const bool tail_ok = !a.pbwd || !GROUPED || a.pm_lo % 64 == 0;
+      if (!a.has_mask && (a.accumulate || a.pbwd) && tail_ok) {
         const int mode = a.pbwd ? (a.accumulate ? EIN_PBACC : EIN_PB) : EIN_ACC;
         if (mode == EIN_ACC)
           kern = al ? pw_fwd_staged_kernel<NCB, NKB, M, false, true, 0, EIN_ACC, H>

@@ -1364,7 +1364,7 @@ extern "C" int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* d, const vsrk_tenso
                                        const float* bias, const vsrk_tensor5* y_fwd, const vsrk_tensor5* y,
                                        int32_t c_lo, float* da, int32_t accumulate_da, void* workspace,
                                        size_t workspace_bytes, void* stream) {
-  VSRK_CHECK(d && x && y && y_fwd && w_packed && d->mask_slope, "conv_fwd_prelu_bwd: null argument");
+  VSRK_CHECK(d && x && y && y_fwd && w_packed && d->mask_slope && da, "conv_fwd_prelu_bwd: null argument");
   VSRK_CHECK(workspace && workspace_bytes >= vsrk_conv_prelu_bwd_workspace(),
              "conv_fwd_prelu_bwd: workspace %zu < %zu bytes", workspace_bytes, vsrk_conv_prelu_bwd_workspace());
   VSRK_CHECK(((uintptr_t)workspace & 15) == 0, "conv_fwd_prelu_bwd: workspace must be 16-byte aligned");
@@ -1387,10 +1387,8 @@ extern "C" int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* d, const vsrk_tenso
   }
   if (rc == 0) return VSRK_ERR_UNSUPPORTED;
   if (rc < 0) return -rc;
-  if (da) {  // (da == NULL: the partials stay in the workspace slot, vsrk_slope_final_sum later)
-    vsrk_slope_final((const double*)workspace, nparts, d->mask_slope, da, accumulate_da, 0, s);
-    VSRK_LAUNCH_CHECK("conv_fwd_prelu_bwd_final");
-  }
+  vsrk_slope_final((const double*)workspace, nparts, d->mask_slope, da, accumulate_da, 0, s);
+  VSRK_LAUNCH_CHECK("conv_fwd_prelu_bwd_final");
   return VSRK_OK;
 }
 

@@ -204,8 +204,8 @@ class _DRFBase(BaseNet):
         reads them (the copy long done by then) to choose, per PReLU, the
         output-based backward (exact while a > 0) or the pre-activation one
         (nn.PReLU's own, any slope; the pre-activation is recomputed from the
-        tape).  Inside graph capture nothing is copied and every PReLU takes
-        the output-based form, whose slope gradient is NaN for a <= 0 (loud)."""
+        tape).  Inside graph capture nothing is copied (the replays may run
+        with other slopes): every PReLU then takes the pre-activation form."""
         if torch.cuda.is_current_stream_capturing():
             return None
         prelus = [m for m in self.modules() if isinstance(m, nn.PReLU)]
@@ -213,7 +213,7 @@ class _DRFBase(BaseNet):
         host = torch.empty(sl.shape, dtype=sl.dtype, pin_memory=True)
         host.copy_(sl, non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record()
+        ev.record(torch.cuda.current_stream(sl.device))  # the stream the copy was queued on
         idx, i = {}, 0
         for m in prelus:
             idx[id(m)] = (i, m.weight.numel())
@@ -332,11 +332,14 @@ class _DRFBase(BaseNet):
         H, W = h * s, w * s
         pw, sp = tape["packer"]
         ib, fb = self.in_block, self.f_block
-        nonpos = set()  # PReLUs with a slope <= 0: the pre-activation backward
+        # PReLUs with a slope <= 0 take the pre-activation backward; so does
+        # every PReLU when the slopes are unknown (graph capture)
         if tape.get("slopes") is not None:
             host, ev, idx = tape["slopes"]
             ev.synchronize()
             nonpos = {k for k, (i, n) in idx.items() if bool((host[i:i + n] <= 0).any())}
+        else:
+            nonpos = {id(m) for m in self.modules() if isinstance(m, nn.PReLU)}
         recs = tape["recs"]
         dev = recs[0]["X0"].device
         if not isinstance(gys, (tuple, list)):
@@ -393,14 +396,23 @@ class _DRFBase(BaseNet):
         # {frame: (x, dy)}, runs launched, frames per run K)
         pend: dict = {}
 
-        def run_frames(x, dy) -> int:
+        run_k: dict = {}  # weight name -> frames per run (tests / bench records)
+        self._seq_run_k = run_k
+        pnames = {id(p_): n_ for n_, p_ in self.named_parameters()}
+
+        def run_frames(x, dy, name="") -> int:
             """K for a weight: the run's view must keep 32-bit element offsets
-            (B x the frame's span of the wider operand, per frame), and runs
-            must not cross a sequence-buffer chunk (K divides Kg)"""
+            (B x the frame's span of the wider operand, per frame).  Runs
+            start at every K-th frame of a sequence-buffer chunk and stop at
+            its end, so K need not divide Kg (round 5 lowered K until it did:
+            at cfg 3, Kg = 13 is prime and the high-res projection weights
+            fell back to single-frame runs)"""
             span = max(v.stride(0) * b for v in (x, dy))
             k_ = max(1, min(Kg, (2 ** 31 - 1) // max(span, 1) - 1))
-            while Kg % k_:
-                k_ -= 1
+            cap = int(os.environ.get("VSR_DRF_RUN_FRAMES", "0"))  # test knob: a shorter run
+            if cap > 0:
+                k_ = min(k_, cap)
+            run_k[name] = k_
             return k_
 
         def launch_runs(t):
@@ -409,10 +421,11 @@ class _DRFBase(BaseNet):
             after its first run)"""
             if not seq:
                 return
+            r0 = (t // Kg) * Kg  # the chunk [r0, r0 + Kg) frame t belongs to
             for key, (prm, launch, frs, nrun, K) in list(pend.items()):
-                if t % K != 0:
+                if (t - r0) % K != 0:
                     continue
-                t1 = min(t + K, T)
+                t1 = min(t + K, r0 + Kg, T)
                 xs = _seq_view([frs[u][0] for u in range(t, t1)])
                 dys = _seq_view([frs[u][1] for u in range(t, t1)])
                 if xs is not None and dys is not None:
@@ -445,7 +458,10 @@ class _DRFBase(BaseNet):
             if not seq:
                 self._on_wgrad_stream(lambda: launch(x, dy, acc), x, dy)
                 return
-            pend.setdefault(id(key), (key, launch, {}, 0, run_frames(x, dy)))[2][t] = (x, dy)
+            ent = pend.get(id(key))
+            if ent is None:
+                ent = pend[id(key)] = (key, launch, {}, 0, run_frames(x, dy, pnames.get(id(key), "")))
+            ent[2][t] = (x, dy)
 
         def wgrad(conv, x, dy, ksz, pad, t, **kw):
             dw, acc = gbuf(conv.weight)
