@@ -378,8 +378,9 @@ int vsrk_conv_pack_weights(int32_t dtype, int32_t n, const vsrk_pack_desc* descs
  * contributor i: dz over depths [d0, d0 + dz.d) of the block and its BN's
  * per-channel operands (pointers at the block's first channel), as in
  * vsrk_bn_relu_bwd_apply.  dx [+]= sum_i apply_i: x and dx move once instead
- * of once per contributor.  1 <= n <= VSRK_BN_MULTI_MAX. */
-#define VSRK_BN_MULTI_MAX 3
+ * of once per contributor.  1 <= n <= VSRK_BN_MULTI_MAX; more than 3
+ * contributors need a block of at most 256 channels. */
+#define VSRK_BN_MULTI_MAX 8
 typedef struct vsrk_bn_contrib {
   vsrk_tensor5 dz;
   int32_t d0;

@@ -115,19 +115,21 @@ def test_duf_dynfilter(dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("ncontrib", [1, 2, 3])
-def test_bn_apply_multi_equals_sequential_applies(dtype, ncontrib):
+@pytest.mark.parametrize("ncontrib,cb", [(1, 32), (2, 32), (3, 32), (4, 32), (6, 32), (7, 64), (8, 20)])
+def test_bn_apply_multi_equals_sequential_applies(dtype, ncontrib, cb):
     """vsrk_bn_relu_bwd_apply_multi (DUF's deferred bn1 input gradients) vs
     the single-contributor apply run once per contributor: every
-    contributor's dz covers its own depth window of the block."""
+    contributor's dz covers its own depth window of the block.  More than
+    three contributors take the one-pass LDS-constant form (DUF's head block
+    has 7, its first unit blocks 4-6); cb = 20: a partial 16-byte chunk (bf16)."""
     g = torch.Generator().manual_seed(11 + ncontrib)
-    n, D, h, w, c, cb = 2, 7, 5, 9, 64, 32
+    n, D, h, w, c = 2, 7, 5, 9, cb + 32
     buf = (torch.randn((n, D, h, w, c + 16), generator=g) * 1.3 + 0.2).to(DEV, dtype)
     x = buf[..., 16:16 + cb]  # the block: a channel slice of a concat buffer
     base = (torch.randn((n, D, h, w, cb), generator=g) * 0.1).to(DEV, dtype)
     cs, seq = [], base.clone()
     for i in range(ncontrib):
-        d0, d1 = [(0, 7), (1, 6), (2, 5)][i]
+        d0, d1 = [(0, 7), (1, 6), (2, 5), (0, 7), (3, 4), (1, 6), (0, 7), (2, 5)][i]
         dz = torch.randn((n, d1 - d0, h, w, c), generator=g).to(DEV, dtype)[..., 8:8 + cb]
         sc = (torch.rand(cb, generator=g) + 0.3).to(DEV)
         sh = torch.randn(cb, generator=g).to(DEV)

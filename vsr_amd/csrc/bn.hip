@@ -424,6 +424,129 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_multi_kernel(View x, Vi
   }
 }
 
+// The same for 4..8 contributors in ONE pass (round 5 split them into passes
+// of three, each re-reading the block's x and dx: DUF's head block took three
+// passes, its first three unit blocks two).  The per-channel constants of
+// every contributor (scale, shift, k1, k2, k3) live in LDS instead of
+// registers (40 floats per contributor and thread would not fit); a row reads
+// each active contributor's five 8-channel groups once for its U voxels.
+// Same fp32 operations in the same contributor order as the register form.
+constexpr int BN_MULTI_LDS_C = 256;  // channels per block the LDS form takes
+template <typename T, int NC>
+__global__ __launch_bounds__(256) void bn_relu_bwd_apply_multi_lds_kernel(View x, View dx, ContribPack<NC> cp,
+                                                                          int nrows, int accumulate) {
+  constexpr int E = Chunk<T>::E;
+  const int C = x.c;
+  const int cpv = (C + E - 1) / E;
+  const int vpb = blockDim.x / cpv;
+  const int ch = threadIdx.x % cpv, vl = threadIdx.x / cpv;
+  const int c0 = ch * E;
+  const bool full = c0 + E <= C;
+  const int CP = cpv * E;  // padded channel count of the tables
+  __shared__ __attribute__((aligned(16))) float cst[NC * 5 * BN_MULTI_LDS_C];  // [i][sc, sh, k1, k2, k3][CP]
+  for (int j = threadIdx.x; j < NC * CP; j += blockDim.x) {
+    const int i = j / CP, cc = j - i * CP;
+    const ContribDev& q = cp.c[i];
+    const int c = min(cc, C - 1);
+    const float is = q.invstd[c], gm = q.gamma ? q.gamma[c] : 1.f;
+    const float a = gm * is, b = is * q.sdyx[c] * q.inv_count;
+    float* t = cst + i * 5 * CP + cc;
+    t[0] = q.scale[c];
+    t[CP] = q.shift[c];
+    t[2 * CP] = a;
+    t[3 * CP] = -a * b;
+    t[4 * CP] = a * (q.mean[c] * b - q.sdy[c] * q.inv_count);
+  }
+  __syncthreads();
+  if (vl >= vpb) return;
+  for (int r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const int h = r % x.h, t = r / x.h, d = t % x.d, n = t / x.d;
+    const T* xr = reinterpret_cast<const T*>(x.ptr) + row_off(x, r) + c0;
+    T* orow = reinterpret_cast<T*>(dx.ptr) + row_off(dx, r) + c0;
+    const T* gr[NC];
+    bool on[NC];
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const ContribDev& q = cp.c[i];
+      on[i] = d >= q.d0 && d < q.d1;
+      gr[i] = reinterpret_cast<const T*>(q.dz.ptr) +
+              (n * q.dz.sn + (int64_t)(on[i] ? d - q.d0 : 0) * q.dz.sd + (int64_t)h * q.dz.sh) + c0;
+    }
+    constexpr int U = BN_MULTI_U;
+    for (int wb = vl; wb < x.w; wb += U * vpb) {
+      uint4 rx[U], ro[U], rg[NC][U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int w = wb + u * vpb;
+        const bool ok = full && w < x.w;
+        rx[u] = ok ? *reinterpret_cast<const uint4*>(xr + (int64_t)w * x.sw) : make_uint4(0, 0, 0, 0);
+        ro[u] = (ok && accumulate) ? *reinterpret_cast<const uint4*>(orow + (int64_t)w * dx.sw)
+                                   : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < NC; ++i)
+          rg[i][u] = (ok && on[i]) ? *reinterpret_cast<const uint4*>(gr[i] + (int64_t)w * cp.c[i].dz.sw)
+                                   : make_uint4(0, 0, 0, 0);
+      }
+      float f[U][E], o[U][E];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int w = wb + u * vpb;
+        if (full) {
+          Chunk<T>::unpack(rx[u], f[u]);
+          Chunk<T>::unpack(ro[u], o[u]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const bool ok = c0 + e < C && w < x.w;
+            f[u][e] = ok ? to_f32<T>(xr[(int64_t)w * x.sw + e]) : 0.f;
+            o[u][e] = (ok && accumulate) ? to_f32<T>(orow[(int64_t)w * dx.sw + e]) : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        if (!on[i]) continue;  // uniform per row
+        float k[5][E];
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+#pragma unroll
+          for (int e = 0; e < E; e += 4)
+            *reinterpret_cast<float4*>(&k[j][e]) = *reinterpret_cast<const float4*>(cst + (i * 5 + j) * CP + c0 + e);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int w = wb + u * vpb;
+          float g[E];
+          if (full) {
+            Chunk<T>::unpack(rg[i][u], g);
+          } else {
+#pragma unroll
+            for (int e = 0; e < E; ++e)
+              g[e] = (c0 + e < C && w < x.w) ? to_f32<T>(gr[i][(int64_t)w * cp.c[i].dz.sw + e]) : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const float dy = fmaf(f[u][e], k[0][e], k[1][e]) > 0.f ? g[e] : 0.f;
+            o[u][e] += fmaf(k[2][e], dy, fmaf(k[3][e], f[u][e], k[4][e]));
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int w = wb + u * vpb;
+        if (w >= x.w) break;
+        T* po = orow + (int64_t)w * dx.sw;
+        if (full) {
+          *reinterpret_cast<uint4*>(po) = Chunk<T>::pack(o[u]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e)
+            if (c0 + e < C) po[e] = from_f32<T>(o[u][e]);
+        }
+      }
+    }
+  }
+}
+
 template <typename T, int NC>
 void launch_apply_multi(const vsrk_tensor5* x, const vsrk_tensor5* dx, int accumulate, const vsrk_bn_contrib* cs,
                         int grid, int thr, int nrows, hipStream_t s) {
@@ -433,7 +556,11 @@ void launch_apply_multi(const vsrk_tensor5* x, const vsrk_tensor5* dx, int accum
     cp.c[i] = ContribDev{make_view(&q.dz), q.d0, q.d0 + q.dz.d, q.scale, q.shift, q.mean, q.invstd, q.gamma,
                          q.sum_dy, q.sum_dy_xhat, (float)(1.0 / q.count)};
   }
-  bn_relu_bwd_apply_multi_kernel<T, NC><<<grid, thr, 0, s>>>(make_view(x), make_view(dx), cp, nrows, accumulate);
+  if constexpr (NC <= 3)
+    bn_relu_bwd_apply_multi_kernel<T, NC><<<grid, thr, 0, s>>>(make_view(x), make_view(dx), cp, nrows, accumulate);
+  else
+    bn_relu_bwd_apply_multi_lds_kernel<T, NC><<<grid, thr, 0, s>>>(make_view(x), make_view(dx), cp, nrows,
+                                                                   accumulate);
 }
 
 // y = x * scale + shift [relu] per channel (the standalone BatchNorm3d forward
@@ -642,6 +769,9 @@ extern "C" int vsrk_bn_relu_bwd_apply_multi(const vsrk_tensor5* x, const vsrk_te
   const int E = vsrk_is16(x->dtype) ? 8 : 4;
   const int cpv = ceil_div(x->c, E);
   VSRK_CHECK(cpv <= 256, "bn_relu_bwd_apply_multi: too many channels (%d)", x->c);
+  VSRK_CHECK(n <= 3 || cpv * E <= BN_MULTI_LDS_C,
+             "bn_relu_bwd_apply_multi: more than 3 contributors need a block of <= %d channels (%d)", BN_MULTI_LDS_C,
+             x->c);
   const int64_t nr64 = (int64_t)x->n * x->d * x->h;
   VSRK_CHECK(nr64 < (1ll << 31), "bn_relu_bwd_apply_multi: too many rows");
   const int nrows = (int)nr64;
@@ -651,9 +781,16 @@ extern "C" int vsrk_bn_relu_bwd_apply_multi(const vsrk_tensor5* x, const vsrk_te
   hipStream_t s = (hipStream_t)stream;
   auto go = [&](auto tag) {
     using T = decltype(tag);
-    if (n == 1) launch_apply_multi<T, 1>(x, dx, accumulate, cs, grid, thr, nrows, s);
-    else if (n == 2) launch_apply_multi<T, 2>(x, dx, accumulate, cs, grid, thr, nrows, s);
-    else launch_apply_multi<T, 3>(x, dx, accumulate, cs, grid, thr, nrows, s);
+    switch (n) {
+      case 1: launch_apply_multi<T, 1>(x, dx, accumulate, cs, grid, thr, nrows, s); break;
+      case 2: launch_apply_multi<T, 2>(x, dx, accumulate, cs, grid, thr, nrows, s); break;
+      case 3: launch_apply_multi<T, 3>(x, dx, accumulate, cs, grid, thr, nrows, s); break;
+      case 4: launch_apply_multi<T, 4>(x, dx, accumulate, cs, grid, thr, nrows, s); break;
+      case 5: launch_apply_multi<T, 5>(x, dx, accumulate, cs, grid, thr, nrows, s); break;
+      case 6: launch_apply_multi<T, 6>(x, dx, accumulate, cs, grid, thr, nrows, s); break;
+      case 7: launch_apply_multi<T, 7>(x, dx, accumulate, cs, grid, thr, nrows, s); break;
+      default: launch_apply_multi<T, 8>(x, dx, accumulate, cs, grid, thr, nrows, s); break;
+    }
   };
   if (x->dtype == VSRK_BF16) go(bf16{});
   else if (x->dtype == VSRK_F16) go(f16{});

@@ -1,3 +1,4 @@
+#include <cstdio>
 // Implicit-GEMM convolution forward / data-gradient on CDNA4 MFMA (gfx950).
 //
 // Replaces the nn.Conv2d / nn.Conv3d forward and backward the reference runs on
@@ -560,12 +561,34 @@ extern "C" int vsrk_conv_fwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, con
   const int NT = y->c <= 32 ? 32 : ((y->c <= 64 || d->kh == 3) ? 64 : 128);
   a.ntn = ceil_div(y->c, NT);
   hipStream_t s = (hipStream_t)stream;
+  // VSRK_LOG_DISPATCH=1: one stderr line per launch -- the path taken and the shapes (diagnostics)
+  static int log_dispatch = -1;
+  if (log_dispatch < 0) {
+    const char* e = getenv("VSRK_LOG_DISPATCH");
+    log_dispatch = (e && e[0] == '1') ? 1 : 0;
+  }
+  auto logd = [&](const char* path) {
+    if (log_dispatch)
+      fprintf(stderr, "vsrk_conv_fwd %s k=%dx%dx%d x=(%d,%d,%d,%d,%d) y=(%d,%d,%d,%d,%d)%s pro=%d act=%d mask=%d res=%d acc=%d\n",
+              path, d->kd, d->kh, d->kw, x->n, x->d, x->h, x->w, x->c, y->n, y->d, y->h, y->w, y->c,
+              ydt == VSRK_F32 ? " f32out" : "", d->prologue, d->act, mask != nullptr, residual != nullptr, d->accumulate);
+  };
   const int pw = vsrk_conv_fwd_pw(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s);
-  if (pw != 0) return pw > 0 ? VSRK_OK : -pw;
+  if (pw != 0) {
+    logd("pw");
+    return pw > 0 ? VSRK_OK : -pw;
+  }
   const int thin = vsrk_conv_fwd_thin(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s);
-  if (thin != 0) return thin > 0 ? VSRK_OK : -thin;
+  if (thin != 0) {
+    logd("thin");
+    return thin > 0 ? VSRK_OK : -thin;
+  }
   const int fast = vsrk_conv_fwd_fast(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s);
-  if (fast != 0) return fast > 0 ? VSRK_OK : -fast;
+  if (fast != 0) {
+    logd("fast");
+    return fast > 0 ? VSRK_OK : -fast;
+  }
+  logd("tile");
   if (xdt == VSRK_BF16) {
     if (ydt == VSRK_BF16) return dispatch_k<bf16, bf16>(a, NT, s);
     return dispatch_k<bf16, float>(a, NT, s);

@@ -516,7 +516,7 @@ def bn_stats_depth(x: torch.Tensor) -> torch.Tensor:
     return out.transpose(0, 1)
 
 
-BN_MULTI_MAX = 3  # VSRK_BN_MULTI_MAX
+BN_MULTI_MAX = 8  # VSRK_BN_MULTI_MAX (more than 3: blocks of <= 256 channels)
 
 
 def bn_relu_bwd_apply_multi(x: torch.Tensor, dx: torch.Tensor, accumulate: bool, contribs) -> torch.Tensor:
