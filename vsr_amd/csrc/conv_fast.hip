@@ -37,6 +37,8 @@ extern "C" int vsrk_conv_set_algo(int32_t mode) {
   return VSRK_OK;
 }
 
+extern int g_pw_wide_mode;  // conv_pw_wide.hip
+
 extern "C" int vsrk_conv_set_path(const char* path, int32_t mode) {
   VSRK_CHECK(path, "conv_set_path: null path");
   const std::string p(path);
@@ -51,6 +53,7 @@ extern "C" int vsrk_conv_set_path(const char* path, int32_t mode) {
   else if (p == "wgrad_row") vsrk_conv_set_wgrad_row_mode(mode);
   else if (p == "roll_wr") vsrk_conv_set_roll_wr_mode(mode);
   else if (p == "stencil") vsrk_conv_set_stencil_mode(mode);
+  else if (p == "pw_wide") g_pw_wide_mode = mode;
   else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, pw, roll, roll_wr, thin, wgrad_pipe, wgrad_roll, wgrad_row, stencil)",
                   path);
   return VSRK_OK;

@@ -573,6 +573,11 @@ extern "C" int vsrk_conv_fwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, con
               path, d->kd, d->kh, d->kw, x->n, x->d, x->h, x->w, x->c, y->n, y->d, y->h, y->w, y->c,
               ydt == VSRK_F32 ? " f32out" : "", d->prologue, d->act, mask != nullptr, residual != nullptr, d->accumulate);
   };
+  const int wide = vsrk_conv_fwd_pw_wide(d, x, w_packed, bias, residual, mask, y, s);
+  if (wide != 0) {
+    logd("pw_wide");
+    return wide > 0 ? VSRK_OK : -wide;
+  }
   const int pw = vsrk_conv_fwd_pw(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s);
   if (pw != 0) {
     logd("pw");

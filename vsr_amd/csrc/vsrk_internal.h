@@ -70,6 +70,10 @@ void vsrk_conv_set_roll_wr_mode(int mode);
 int vsrk_conv_fwd_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
                      const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                      const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s);
+// wide pointwise convs (conv_pw_wide.hip: > 256 input channels or 256 -> >= 256)
+int vsrk_conv_fwd_pw_wide(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                          const vsrk_tensor5* residual, const vsrk_tensor5* mask, const vsrk_tensor5* y,
+                          hipStream_t s);
 int vsrk_conv_fwd_pw_pbwd(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed,
                           const vsrk_tensor5* mask, const vsrk_tensor5* y, int c_lo, const vsrk_slope_out* slope,
                           hipStream_t s);
