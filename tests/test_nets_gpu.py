@@ -110,6 +110,7 @@ def _psnr(out, hr):
 CASES = ["edsr_x4_small", "edsr_x3_small", "edsr_x2_cfg1", "edsr_x4_canon", "duf_x4_canon", "drf_x4_canon",
          "drf_sisr_x2_small", "duf_x4_cond", "drf_x4_cond"]
 COND = {"duf_x4_cond", "drf_x4_cond"}
+FP16_OUT_EPS = 1e-3  # EDSR fixtures: fp16 output max|d| against fp64 (canon: 4.5e-4)
 
 
 def _proj(t, key, n):
@@ -147,6 +148,8 @@ def test_net_matches_golden(name, precision):
         assert d.max().item() <= max(1e-4, 3 * fx["out_err32"]), d.max().item()
     elif precision == "fp16":
         assert d.max().item() <= 5e-3 and d.mean().item() <= 5e-4, (d.max().item(), d.mean().item())
+        if name.startswith("edsr"):  # (bounds the tail-bias sign-flip allowance below)
+            assert d.max().item() <= FP16_OUT_EPS, d.max().item()
     else:
         assert d.max().item() <= 3e-2 and d.mean().item() <= 3e-3, (d.max().item(), d.mean().item())
     assert abs(_psnr([o.detach() for o in out] if isinstance(out, list) else out.detach(), hr).item()
@@ -169,48 +172,49 @@ def test_net_matches_golden(name, precision):
             tol = max(3e-2, 3 * fx["fp16_env"][k])
         else:
             tol = max(8e-2, 2 * fx["bf16_env"][k])
-        if precision != "fp32" and k == "tail.conv.bias" and not isinstance(out, list):
-            # the bias of the conv feeding the L1 loss gets sum_v sign(o_v - hr_v) / N:
-            # a residual within the output's own 16-bit error of zero can flip
-            # (2 / N each) for ANY implementation at this precision -- the 16-bit
-            # envelope's draws happened to flip none on some fixtures.  Only the
-            # residuals that DID flip in this run widen the bound, by exactly
-            # their 2 / N each (not every residual within the run's
-            # global max error), and never by more than the residuals within
-            # the precision's ALLOWED output error (asserted above) could flip;
-            # the run with the 16-bit stencil tail off must meet the plain bound
-            # (test_tail_bias_without_stencil_meets_envelope)
+        if precision == "fp16" and k == "tail.conv.bias" and not isinstance(out, list):
+            # The bias of the conv feeding the L1 loss gets sum_v sign(o_v - hr_v) / N,
+            # and on these fixtures the signs nearly cancel (edsr_x4_canon: N = 6144,
+            # |grad| = 2.3e-3), so one residual flipping sign moves the gradient by
+            # 2 / N / |grad| = 14 % -- a residual the 16-bit output error can flip for
+            # ANY implementation at this precision (canon: the flip is a residual of
+            # 4.4e-5 against an fp16 output rms error of 8.9e-5, stencil and tile tail
+            # kernels alike: tools/diag/tailbias_fp16.py, profiles/r6_tailbias_fp16.txt);
+            # the ideal-16-bit envelope's four draws happened to flip none.  Fixed,
+            # fixture-derived allowance: every fixture residual within FP16_OUT_EPS
+            # (the fp16 output bound asserted above for the EDSR fixtures) may flip.
             o64, h64 = _flat(fx["output64"]).double(), _flat(fx["hr"]).double()
-            flips = ((got - h64).sign() != (o64 - h64).sign()).sum().item()
-            allowed = 5e-3 if precision == "fp16" else 3e-2
-            near = ((o64 - h64).abs() <= allowed).sum().item()
+            near = ((o64 - h64).abs() <= FP16_OUT_EPS).sum().item()
             ref_b = fx["grad_full64"][k].double().norm().item() if k in fx["grad_full64"] else None
             if ref_b:
-                tol += 2.0 * min(flips, near) / o64.numel() / ref_b
+                tol += 2.0 * near / o64.numel() / ref_b
         assert rel <= tol, (k, rel, tol)
 
 
 @pytest.mark.parametrize("precision", ["bf16", "fp16"])
 @pytest.mark.parametrize("name", [c for c in CASES if c.startswith("edsr")])
-def test_tail_bias_without_stencil_meets_envelope(name, precision):
-    """The EDSR tail bias gradient with the one-channel stencil tail kernels
-    off (the tile kernels round every residual as round 3 did) stays within the
-    16-bit envelope with no sign-flip allowance."""
+def test_stencil_tail_output_error_matches_tile_path(name, precision):
+    """the one-channel stencil tail kernels' 16-bit output
+    error against fp64 is no larger than the tile kernels' (stencil off) on
+    every EDSR fixture -- max and rms per voxel within 10 % -- so a residual
+    sign flip on the tail bias gradient is the precision's, not the kernel's
+    (see the FP16_OUT_EPS allowance in test_net_matches_golden)."""
     fx = load_golden(name)
-    F.set_conv_path("stencil", 0)
-    try:
-        net = _build(fx, precision)
-        lr, hr = _to(fx["lr"]), _to(fx["hr"])
-        out = net(lr)
-        _l1(out, hr).backward()
-        torch.cuda.synchronize()
-    finally:
-        F.set_conv_path("stencil", -1)
-    k = "tail.conv.bias"
-    g = dict(net.named_parameters())[k].grad.detach().cpu().double()
-    tol = max(3e-2, 3 * fx["fp16_env"][k]) if precision == "fp16" else max(8e-2, 2 * fx["bf16_env"][k])
-    rel = _rel(g, fx, k)
-    assert rel <= tol, (k, rel, tol)
+    exp = _flat(fx["output64"]).double()
+    stats = []
+    for mode in (1, 0):
+        F.set_conv_path("stencil", mode)
+        try:
+            net = _build(fx, precision)
+            with torch.no_grad():
+                out = net(_to(fx["lr"]))
+            torch.cuda.synchronize()
+        finally:
+            F.set_conv_path("stencil", -1)
+        d = _flat(out).detach().cpu().double() - exp
+        stats.append((d.abs().max().item(), d.pow(2).mean().sqrt().item()))
+    (mx_s, rms_s), (mx_t, rms_t) = stats
+    assert mx_s <= 1.1 * mx_t and rms_s <= 1.1 * rms_t, stats
 
 
 def test_cond_fixtures_are_well_conditioned():
