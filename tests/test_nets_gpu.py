@@ -34,7 +34,7 @@ fp16 HIP path (loss-scaled backward, BaseNet._loss_scale): output max |d| <=
   2^18 does not move it); on edsr_x4_canon it tracks the envelope (2-3e-2 vs
   1.5-3e-2, tools/diag/f16_edsr.py), hence the 3x multiplier.
 bf16 HIP path: output max |d| <= 3e-2, mean |d| <= 3e-3; gradient rel-L2 <=
-  max(8e-2, 2*bf16_env) where bf16_env is the error of an *ideal*
+  max(5e-2, 2*bf16_env) (round 6; 8e-2 before) where bf16_env is the error of an *ideal*
   bf16-storage implementation (fp64 math, bf16 weights, every conv/BN output
   and input gradient rounded to bf16; worst of 4 dithered draws, in the
   fixture).  Every layer stores activations and data-gradients in bf16
@@ -171,7 +171,7 @@ def test_net_matches_golden(name, precision):
         elif precision == "fp16":
             tol = max(3e-2, 3 * fx["fp16_env"][k])
         else:
-            tol = max(8e-2, 2 * fx["bf16_env"][k])
+            tol = max(5e-2, 2 * fx["bf16_env"][k])
         if precision == "fp16" and k == "tail.conv.bias" and not isinstance(out, list):
             # The bias of the conv feeding the L1 loss gets sum_v sign(o_v - hr_v) / N,
             # and on these fixtures the signs nearly cancel (edsr_x4_canon: N = 6144,
