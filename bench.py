@@ -68,6 +68,7 @@ from vsr_amd.losses import L1Loss  # noqa: E402
 
 METRIC = "voxels/sec fwd+bwd, 4× SR on 16×128×128 cine volumes, 1/2/4/8 MI355X"
 PEAK = {"bf16": 2.5e15, "fp16": 2.5e15, "fp32": 157.3e12}
+HBM_PEAK = 8.0e12  # MI355X HBM3E spec (MI355X_MICROARCH.md; ~6.3e12 achievable)
 B, T, H, W, R = 4, 16, 128, 128, 4
 DATASET = "acdc"  # synthetic-data normalisation: "acdc", "dsb15" or "mixed" (half the volumes each)
 # BASELINE.json configs measurable on one node (--config): the batch / frames /
@@ -344,9 +345,14 @@ def run_model(name, args, world, rank, dev):
     by_dir = {}  # fwd / dgrad / wgrad launches of the roofline kernel on their own
     for lab in F.timer.labels():
         f_, t_, n_ = F.timer.totals(lab)
+        tb_, _, b_ = F.timer.bound_seconds(PEAK[args.precision], HBM_PEAK, lab)
         by_dir[lab] = {"ms_per_step": t_ / tsteps * 1e3, "launches_per_step": n_ / tsteps,
                        "tflop_per_step": f_ / tsteps / 1e12,
-                       "frac": (f_ / t_ / PEAK[args.precision]) if t_ > 0 else None}
+                       "frac": (f_ / t_ / PEAK[args.precision]) if t_ > 0 else None,
+                       "gb_per_step": b_ / tsteps / 1e9, "bound_frac": (tb_ / t_) if t_ > 0 else None}
+    # each launch priced at max(FLOP / MFMA peak, algorithmic bytes / HBM peak):
+    # the honest roofline of a conv near the ridge (EDSR's 64 -> 64 body convs)
+    tb, tmf, bytes_ = F.timer.bound_seconds(PEAK[args.precision], HBM_PEAK)
     F.timer = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
@@ -367,11 +373,26 @@ def run_model(name, args, world, rank, dev):
                    "parallelism": f"dp{world}" + ("+syncbn" if world > 1 and name == "duf" else "")},
         "roofline": {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None, "peak": peak / 1e12,
                      "unit": "TFLOP/s", "frac": achieved / peak if achieved else None, "traffic": traffic,
+                     "mfma_frac": achieved / peak if achieved else None,
                      "traffic_kernel": tkern, "kernel": kdesc,
                      "kernel_ms_per_step": kernel_s / tsteps * 1e3, "launches_per_step": launches / tsteps,
-                     "flop_per_step": flop / tsteps, "by_direction": by_dir},
+                     "flop_per_step": flop / tsteps, "by_direction": by_dir,
+                     "bytes_per_step": bytes_ / tsteps, "hbm_peak_tbs": HBM_PEAK / 1e12,
+                     "bound_ms_per_step": tb / tsteps * 1e3,
+                     "bound_frac": (tb / kernel_s) if kernel_s > 0 else None,
+                     "bound_mix": {"mfma_ms_per_step": tmf / tsteps * 1e3,
+                                   "hbm_ms_per_step": (tb - tmf) / tsteps * 1e3},
+                     "bound_note": "bound_frac = sum over launches of max(FLOP/MFMA peak, algorithmic bytes/HBM "
+                                   "peak) / measured time; frac prices FLOP alone"},
         "final_loss": float(loss.item()),
     }
+    rf = res["roofline"]
+    if kernel_s > 0 and tb - tmf > tmf:
+        # the launches are HBM-bound by their algorithmic bytes (EDSR's 64 -> 64
+        # body convs: 268-402 MB per launch, 34-50 us at 8 TB/s against 31 us
+        # of MFMA work): the roofline is the HBM one
+        rf.update(bound="hbm", achieved=bytes_ / kernel_s / 1e9, peak=HBM_PEAK / 1e9, unit="GB/s",
+                  frac=bytes_ / kernel_s / HBM_PEAK)
     if comm is not None:
         res["comm"] = comm
     if getattr(net, "_seq_run_k", None):  # DRF: frames per sequence-buffer chunk and per weight-gradient run
@@ -418,7 +439,8 @@ def worker(args, world, rank, local):
             for m in names:
                 rf = results[m]["roofline"]
                 if rf["achieved"]:
-                    rf["frac_of_measured_peak"] = rf["achieved"] / pk["mfma_bf16_tflops"]
+                    rf["frac_of_measured_peak"] = (rf["achieved"] / pk["mfma_bf16_tflops"] if rf["unit"] == "TFLOP/s"
+                                                   else rf["achieved"] / (pk["hbm_copy_tbs"] * 1e3))
         if "duf" in results:
             # BASELINE.json north_star: ">= 50 % of CDNA4 bf16 MFMA roofline on the
             # 3x3x3 conv fwd+bwd at batch 4x16x128x128" -- the DUF line's roofline

@@ -41,15 +41,19 @@ class KernelTimer:
     a roofline kernel goes through ``wrap`` -- the plain conv, the fused conv +
     reduction (conv_reduce) and the fused conv + PReLU backward
     (conv_prelu_bwd) -- so a fused data gradient is timed like the unfused one.
-    bench.py uses it for the roofline of the dominant conv."""
+    bench.py uses it for the roofline of the dominant conv.  Each launch also
+    carries its algorithmic HBM bytes (``view_bytes`` of the operands it reads
+    and writes once: x and y, plus the residual / mask / accumulate / BN-input
+    operands the caller passes as ``extra``), so the roofline can price a
+    launch at max(FLOP / MFMA peak, bytes / HBM peak) (``bound_seconds``)."""
 
     def __init__(self, match):
         self.match = match
-        self.events: list[tuple[torch.cuda.Event, torch.cuda.Event, float, str]] = []
+        self.events: list[tuple[torch.cuda.Event, torch.cuda.Event, float, str, float]] = []
         self.enabled = True
         self.phase = "fwd"
 
-    def wrap(self, kind, xv, yv, launch, launched=lambda rc: True):
+    def wrap(self, kind, xv, yv, launch, launched=lambda rc: True, extra: float = 0.0):
         """launch() -> status; ``launched(status)`` False means nothing ran
         (a fused entry point reporting "not eligible"): the events are dropped."""
         flop = self.match(kind, xv, yv) if self.enabled else 0
@@ -61,15 +65,24 @@ class KernelTimer:
         e.record()
         if launched(out):
             label = "wgrad" if kind[0] == "conv_wgrad" else ("dgrad" if self.phase == "bwd" else "fwd")
-            self.events.append((s, e, float(flop), label))
+            self.events.append((s, e, float(flop), label, view_bytes(xv) + view_bytes(yv) + float(extra)))
         return out
 
     def totals(self, label: str | None = None) -> tuple[float, float, int]:
         """(total FLOP, total seconds, launches) of the matched launches [of one direction]."""
         torch.cuda.synchronize()
         ev = [x for x in self.events if label is None or x[3] == label]
-        t = sum(s.elapsed_time(e) for s, e, _, _ in ev) * 1e-3
-        return sum(f for _, _, f, _ in ev), t, len(ev)
+        t = sum(x[0].elapsed_time(x[1]) for x in ev) * 1e-3
+        return sum(x[2] for x in ev), t, len(ev)
+
+    def bound_seconds(self, mfma_peak: float, hbm_peak: float, label: str | None = None) -> tuple[float, float, float]:
+        """(sum over launches of max(FLOP / mfma_peak, bytes / hbm_peak), the
+        MFMA part of that sum, total bytes) -- the roofline time of the
+        matched launches [of one direction]."""
+        ev = [x for x in self.events if label is None or x[3] == label]
+        tb = sum(max(x[2] / mfma_peak, x[4] / hbm_peak) for x in ev)
+        tm = sum(x[2] / mfma_peak for x in ev if x[2] / mfma_peak >= x[4] / hbm_peak)
+        return tb, tm, sum(x[4] for x in ev)
 
     def labels(self) -> list[str]:
         return [d for d in ("fwd", "dgrad", "wgrad") if any(x[3] == d for x in self.events)]
@@ -80,6 +93,11 @@ class KernelTimer:
 
 
 timer: KernelTimer | None = None
+
+
+def view_bytes(v) -> float:
+    """Bytes of a logical view (vsrk_tensor5): voxels x channels x element size."""
+    return float(v.n) * v.d * v.h * v.w * v.c * (4 if v.dtype == N.VSRK_F32 else 2)
 
 
 def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
@@ -204,7 +222,12 @@ def conv(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, *, bias: to
                                  N.ptr(pro_shift), C.byref(rv) if rv is not None else None,
                                  C.byref(mv) if mv is not None else None, C.byref(yv), N.stream_ptr(x.device))
 
-    rc = timer.wrap(("conv_fwd", tuple(k)), xv, yv, launch) if timer is not None else launch()
+    if timer is not None:
+        extra = (view_bytes(rv) if rv is not None else 0.0) + (view_bytes(mv) if mv is not None else 0.0) + (
+            view_bytes(yv) if accumulate else 0.0)
+        rc = timer.wrap(("conv_fwd", tuple(k)), xv, yv, launch, extra=extra)
+    else:
+        rc = launch()
     N.check(rc, "conv_fwd")
     return y
 
@@ -238,7 +261,8 @@ def conv_prelu_bwd(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, y
                                            int(c_lo), da.data_ptr(),
                                            1 if accumulate_da else 0, ws.data_ptr(), nbytes, N.stream_ptr(y.device))
 
-    rc = (timer.wrap(("conv_fwd", tuple(k)), xv, yv, launch, _launched) if timer is not None else launch())
+    rc = (timer.wrap(("conv_fwd", tuple(k)), xv, yv, launch, _launched,
+                     extra=view_bytes(mv) + (view_bytes(yv) if accumulate else 0.0)) if timer is not None else launch())
     if rc == 2:  # VSRK_ERR_UNSUPPORTED
         return False
     N.check(rc, "conv_fwd_prelu_bwd")
@@ -275,7 +299,8 @@ def conv_reduce(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, *, bias: tor
                                         out[0].data_ptr(), out[1].data_ptr(), ws.data_ptr(), ws.numel(),
                                         N.stream_ptr(y.device))
 
-    rc = (timer.wrap(("conv_fwd", tuple(k)), xv, yv, launch, _launched) if timer is not None else launch())
+    rc = (timer.wrap(("conv_fwd", tuple(k)), xv, yv, launch, _launched,
+                     extra=view_bytes(bv) if bv is not None else 0.0) if timer is not None else launch())
     if rc == 2:  # VSRK_ERR_UNSUPPORTED
         return None
     N.check(rc, "conv_fwd_reduce")
