@@ -75,8 +75,12 @@ def test_rccl_one_rank_equals_no_group(precision):
     tol = 1e-5 if precision == "fp32" else 1e-2
     assert abs(got["out"] - ref["out"]).max() <= tol * (1 + abs(ref["out"]).max())
     gmax = max(float((v ** 2).sum()) ** 0.5 for v in ref["grads"].values())
+    # (floor: the conv biases in front of a BatchNorm -- every DUF conv bias --
+    # have an exactly zero gradient; both runs' values are summation noise of
+    # size ~1e-5 gmax in bf16, so they are compared at an absolute floor)
+    floor = 1e-3 if precision == "fp32" else 1e-2
     for k, v in ref["grads"].items():
         d = float(((got["grads"][k] - v) ** 2).sum()) ** 0.5
-        assert d <= tol * max(float((v ** 2).sum()) ** 0.5, 1e-3 * gmax), (k, d)
+        assert d <= tol * max(float((v ** 2).sum()) ** 0.5, floor * gmax), (k, d)
     for k, v in ref["buffers"].items():
         assert abs(got["buffers"][k] - v).max() <= tol * (1 + abs(v).max()), k
