@@ -50,8 +50,16 @@ typedef uint32_t roll_u32x4 __attribute__((ext_vector_type(4)));
 namespace {
 using namespace vsrk_conv;
 
-constexpr int RNW = 8;                     // waves (2 per SIMD)
-constexpr int RMS = 2;                     // output rows per wave
+// waves per workgroup and output rows per wave (A/B builds: -DROLL_RNW=4
+// -DROLL_RMS=4 keeps the 16-row tile with one wave per SIMD)
+#ifndef ROLL_RNW
+#define ROLL_RNW 8
+#endif
+#ifndef ROLL_RMS
+#define ROLL_RMS 2
+#endif
+constexpr int RNW = ROLL_RNW;              // waves (2 per SIMD)
+constexpr int RMS = ROLL_RMS;              // output rows per wave
 constexpr int RFTH = RNW * RMS;            // 16 tile rows
 constexpr int RHW = TW + 2;                // 34 halo columns
 constexpr int RHROWS = (RFTH + 2) * RHW;   // 612 halo voxels
@@ -102,10 +110,15 @@ struct RollGeo {
   // 48 KB / 40 KB: A | B | junk pieces.  WR: 24 KB (2-D: the transposed
   // epilogue parks a row in two halves, 2 KB per wave) or 32 KB (3-D: room
   // for the one-pass 4 KB park; the fourth piece per wave is never loaded)
-  static constexpr int SLOT = (WR && KD == 3 ? 4 : NQ) * RNW * 1024;
+  static constexpr int SLOT = (WR && KD == 3 && NQ < 4 ? 4 : NQ) * RNW * 1024;
+  static constexpr int PPW = SLOT / (RNW * 1024);  // slot pieces per wave (the epilogue's park scratch)
   static constexpr int NACC = KD * NT;             // accumulator sets: banks (KD 3) or blocks (KD 1)
   static constexpr int NG = 3 * NACC;              // compute groups (kw, set): 9 / 6
-  static constexpr int NTG = NG - NQ;              // groups that carry the late prologue: 3 / 1
+  // groups 0 .. NDG-1 issue the next-but-one stage's pieces, PPG each; the
+  // rest carry the late prologue (8 waves: one piece per group)
+  static constexpr int NDG = NQ < NG - 1 ? NQ : NG - 1;
+  static constexpr int PPG = (NQ + NDG - 1) / NDG;
+  static constexpr int NTG = NG - NDG;             // groups that carry the late prologue: 3 / 1
   static constexpr int TPG = (RNA + NTG - 1) / NTG;
   static_assert(NTG >= 1, "a group must be left for the late prologue");
 };
@@ -196,7 +209,7 @@ __device__ __forceinline__ void roll_wait_vmcnt() {
 }
 
 template <int KD, int NT, int PRO, int EM, int SP, typename H, int WR>
-__global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
+__global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a) {
   static_assert(SP == SP_NONE || KD == 1, "sub-pixel views: 2-D form only");
   static_assert(!WR || SP == SP_NONE, "resident weights: plain views only");
   using G = RollGeo<KD, NT, WR>;
@@ -204,9 +217,9 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
   // the transposed epilogue parks a row in two halves (2 KB of scratch per
   // wave) where the slot is too small for one 4 KB park (WR)
 #ifdef ROLL_PARK2
-  constexpr bool PARK2 = ROLL_PARK2 || (WR && KD == 1);
+  constexpr bool PARK2 = ROLL_PARK2 || G::PPW < 4;
 #else
-  constexpr bool PARK2 = WR && KD == 1;
+  constexpr bool PARK2 = G::PPW < 4;
 #endif
   // the residual / mask operand of a 2-D tile is loaded into registers during
   // its last stage (one extra operand, no accumulate)
@@ -542,15 +555,20 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       const int kw = g / NACC, b = g % NACC;
       if (g + 1 < G::NG) load_b(bw[(g + 1) & 1], g + 1);
       if (b == (NACC == 3 ? 1 : 0) && kw + 1 < 3) load_a(ax[(kw + 1) & 1], kw + 1);
-      if (g < RNQ && (ROLL_LEAN || don)) dma(dn, g, (SLOT + 2) % 3);
+      if (g < G::NDG && (ROLL_LEAN || don)) {
+#pragma unroll
+        for (int pp = 0; pp < G::PPG; ++pp)
+          if (g * G::PPG + pp < RNQ) dma(dn, g * G::PPG + pp, (SLOT + 2) % 3);
+      }
       if constexpr (PRO) {
-        if (g == RNQ && tnext) {
+        if (g == G::NDG && tnext) {
           if (ROLL_LEAN || don) roll_wait_vmcnt<RNQ>();  // the next stage's pieces landed (the one after stays in flight)
           else roll_wait_vmcnt<0>();
         }
-        if (g >= RNQ && tnext) {
+        if (g >= G::NDG && tnext) {
 #pragma unroll
-          for (int q = (g - RNQ) * G::TPG; q < (g - RNQ + 1) * G::TPG && q < RNA; ++q) transform_piece(sl1, q, tc, tm);
+          for (int q = (g - G::NDG) * G::TPG; q < (g - G::NDG + 1) * G::TPG && q < RNA; ++q)
+            transform_piece(sl1, q, tc, tm);
         }
       }
       if ((bm >> b) & 1) {
@@ -629,7 +647,7 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
       if constexpr (!PARK2) {
 #pragma unroll
         for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<float4*>(ws + (r >> 3) * 8 * 1024 + (r & 7) * 128 + (((2 * g + hf) ^ (r & 7)) * 16)) =
+          *reinterpret_cast<float4*>(ws + (r >> 3) * RNW * 1024 + (r & 7) * 128 + (((2 * g + hf) ^ (r & 7)) * 16)) =
               make_float4(A[ms][4 * g], A[ms][4 * g + 1], A[ms][4 * g + 2], A[ms][4 * g + 3]);
       }
 #pragma unroll
@@ -637,11 +655,11 @@ __global__ __launch_bounds__(RNW * 64, 2) void conv_roll_kernel(RollArgs a) {
         if (PARK2 && (r >> 4) == k) {  // this half's 16 voxels park their 32 channels
 #pragma unroll
           for (int g = 0; g < 4; ++g)
-            *reinterpret_cast<float4*>(ws + ((r >> 3) & 1) * 8 * 1024 + (r & 7) * 128 + (((2 * g + hf) ^ (r & 7)) * 16)) =
+            *reinterpret_cast<float4*>(ws + ((r >> 3) & 1) * RNW * 1024 + (r & 7) * 128 + (((2 * g + hf) ^ (r & 7)) * 16)) =
                 make_float4(A[ms][4 * g], A[ms][4 * g + 1], A[ms][4 * g + 2], A[ms][4 * g + 3]);
         }
         const int v = tv + 16 * k, wo = tl.w0 + v;
-        const char* rb = PARK2 ? ws + (tv >> 3) * 8 * 1024 + (tv & 7) * 128 : ws + (v >> 3) * 8 * 1024 + (v & 7) * 128;
+        const char* rb = PARK2 ? ws + (tv >> 3) * RNW * 1024 + (tv & 7) * 128 : ws + (v >> 3) * RNW * 1024 + (v & 7) * 128;
         const float4 q0 = *reinterpret_cast<const float4*>(rb + (((2 * tc8) ^ (v & 7)) * 16));
         const float4 q1 = *reinterpret_cast<const float4*>(rb + (((2 * tc8 + 1) ^ (v & 7)) * 16));
         float t[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
