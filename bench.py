@@ -288,6 +288,24 @@ def metric_report(net, x, y, dev, iters=10):
     return res
 
 
+def write_units(path, model, precision, rows):
+    """Per-launch table of the roofline kernel (one step, launch order): the
+    per-unit north-star table (DUF: 6 dense units x fwd / dgrad / wgrad)."""
+    if not rows:
+        return
+    tot_us = sum(r["us"] for r in rows)
+    tot_f = sum(r["gflop"] for r in rows)
+    with open(path, "a") as f:
+        f.write(f"# {model} {precision}: {len(rows)} launches per step, {tot_us / 1e3:.3f} ms, "
+                f"{tot_f / 1e3:.3f} TFLOP, frac {tot_f * 1e9 / (tot_us * 1e-6) / PEAK[precision]:.3f} of "
+                f"{PEAK[precision] / 1e15:.1f} PF; bound = max(FLOP / MFMA peak, bytes / {HBM_PEAK / 1e12:.0f} TB/s)\n")
+        f.write(f"{'pos':>3} {'dir':<6} {'shape (taps cin x D -> cout x D @ n x h x w)':<44} {'us':>8} {'GFLOP':>8} "
+                f"{'MB':>8} {'frac':>6} {'TB/s':>6} {'bound':>6}\n")
+        for r in rows:
+            f.write(f"{r['pos']:>3} {r['dir']:<6} {r['shape']:<44} {r['us']:>8.1f} {r['gflop']:>8.1f} {r['mb']:>8.1f} "
+                    f"{r['frac']:>6.3f} {r['hbm_frac'] * HBM_PEAK / 1e12:>6.2f} {r['bound_frac']:>6.3f}\n")
+
+
 def run_model(name, args, world, rank, dev):
     spec = MODELS[name]
     torch.manual_seed(0)  # identical initial weights on every rank
@@ -353,6 +371,8 @@ def run_model(name, args, world, rank, dev):
     # each launch priced at max(FLOP / MFMA peak, algorithmic bytes / HBM peak):
     # the honest roofline of a conv near the ridge (EDSR's 64 -> 64 body convs)
     tb, tmf, bytes_ = F.timer.bound_seconds(PEAK[args.precision], HBM_PEAK)
+    if args.units and rank == 0:
+        write_units(args.units, name, args.precision, F.timer.per_launch(tsteps, PEAK[args.precision], HBM_PEAK))
     F.timer = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
@@ -494,6 +514,7 @@ def main():
     ap.add_argument("--precision", default=None, choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-peaks", action="store_true", help="skip the measured MFMA / HBM peak microbenchmarks")
+    ap.add_argument("--units", default=None, help="append the roofline kernel's per-launch table (one step) to FILE")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     args.models = args.model or args.models or cfg["models"]

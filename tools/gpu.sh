@@ -51,7 +51,7 @@ for STEP in "$@"; do
       [ -n "$A2" ] && EXTRA="--models $A2"
       [ $KIND = quick ] && EXTRA="$EXTRA --steps 5 --warmup 2 --no-cpu-baseline --no-peaks"
       F=$O.$KIND.$CFG${A2:+.${A2//,/_}}
-      timeout -k 10 900 python bench.py --config $CFG $EXTRA > $F.json 2> $F.err || { tail -20 $F.err; exit 1; }
+      timeout -k 10 900 python bench.py --config $CFG $EXTRA --units $F.units.txt > $F.json 2> $F.err || { tail -20 $F.err; exit 1; }
       summary $F.json ;;
     prof)
       CFG=${A1:-cfg2}; M=${A2:-duf}; D=$R/$O.prof_${CFG}_${M//,/_}

@@ -49,7 +49,7 @@ class KernelTimer:
 
     def __init__(self, match):
         self.match = match
-        self.events: list[tuple[torch.cuda.Event, torch.cuda.Event, float, str, float]] = []
+        self.events: list[tuple[torch.cuda.Event, torch.cuda.Event, float, str, float, str]] = []
         self.enabled = True
         self.phase = "fwd"
 
@@ -65,7 +65,8 @@ class KernelTimer:
         e.record()
         if launched(out):
             label = "wgrad" if kind[0] == "conv_wgrad" else ("dgrad" if self.phase == "bwd" else "fwd")
-            self.events.append((s, e, float(flop), label, view_bytes(xv) + view_bytes(yv) + float(extra)))
+            self.events.append((s, e, float(flop), label, view_bytes(xv) + view_bytes(yv) + float(extra),
+                                _launch_desc(kind, xv, yv)))
         return out
 
     def totals(self, label: str | None = None) -> tuple[float, float, int]:
@@ -84,6 +85,28 @@ class KernelTimer:
         tm = sum(x[2] / mfma_peak for x in ev if x[2] / mfma_peak >= x[4] / hbm_peak)
         return tb, tm, sum(x[4] for x in ev)
 
+    def per_launch(self, steps: int, mfma_peak: float, hbm_peak: float) -> list[dict]:
+        """The matched launches by position within a step (the step's launch
+        order is fixed): mean time, FLOP, bytes, MFMA and bound fractions --
+        the per-unit table of the roofline kernel.  [] if the launch count is
+        not a multiple of ``steps``."""
+        torch.cuda.synchronize()
+        n = len(self.events)
+        if steps <= 0 or n % steps:
+            return []
+        per = n // steps
+        rows = []
+        for i in range(per):
+            ev = self.events[i::per]
+            t = sum(x[0].elapsed_time(x[1]) for x in ev) * 1e-3 / len(ev)
+            f, b = ev[0][2], ev[0][4]
+            tb = max(f / mfma_peak, b / hbm_peak)
+            rows.append({"pos": i, "dir": ev[0][3], "shape": ev[0][5], "us": t * 1e6, "gflop": f / 1e9,
+                         "mb": b / 1e6, "frac": f / t / mfma_peak if t > 0 else None,
+                         "hbm_frac": b / t / hbm_peak if t > 0 else None,
+                         "bound_frac": tb / t if t > 0 else None})
+        return rows
+
     def labels(self) -> list[str]:
         return [d for d in ("fwd", "dgrad", "wgrad") if any(x[3] == d for x in self.events)]
 
@@ -93,6 +116,13 @@ class KernelTimer:
 
 
 timer: KernelTimer | None = None
+
+
+def _launch_desc(kind, xv, yv) -> str:
+    """Launch shape for the per-unit table: kernel taps, channels x depth of
+    the input (weight gradient: the input and the output gradient) and output."""
+    k = "x".join(str(i) for i in kind[1])
+    return f"{k} {xv.c}x{xv.d}->{yv.c}x{yv.d} @{xv.n}x{xv.h}x{xv.w}"
 
 
 def view_bytes(v) -> float:
