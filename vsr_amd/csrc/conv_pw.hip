@@ -26,6 +26,7 @@
 //    (deterministic).  One pass over dY and X per cin/cout chunk.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 #include "conv_common.h"
 
 int vsrk_g_pw_mode = -1;  // -1: from VSRK_CONV_PW (default on), 0 off, 1 on
@@ -909,12 +910,24 @@ struct PwWArgs {
   int want_bias;
 };
 
-// NCO dY channel blocks per chunk; wave w owns X blocks w, w+4 (NCIW of them).
-template <int NCO, int NCIW, typename H>
-__global__ __launch_bounds__(PW_THR, 1) void pw_wgrad_kernel(PwWArgs a) {
+// NCO dY channel blocks per chunk; NW waves (4 or 8), wave w owns X blocks
+// w, w + NW, ... (NCIW of them).  NW = 8 takes the wide chunks (5-8 X
+// blocks) with one block per wave: one pass over dY at 160-256 channels and
+// half the accumulators per wave of the 4-wave form's two blocks.
+// DEPTH register-staged stages in flight: 1 = the next stage's loads overlap
+// the current stage's MFMAs only; 2 = two stages ahead (twice the staging
+// registers).  A stage is 64 voxels, a few microseconds of HBM latency
+// against well under one of MFMA work at these channel counts, so one
+// stage in flight leaves the workgroup waiting on its loads (2.4-3 TB/s at
+// 160-224 channels).
+template <int NCO, int NCIW, typename H, int DEPTH = 1, int NW = 4>
+__global__ __launch_bounds__(NW * 64, 1) void pw_wgrad_kernel(PwWArgs a) {
   const H* aX = reinterpret_cast<const H*>(a.x);
   const H* aD = reinterpret_cast<const H*>(a.dy);
-  constexpr int NCIMAX = 4 * NCIW;
+  constexpr int THR = NW * 64;
+  constexpr int NCIMAX = NW * NCIW;
+  constexpr int DK = (PW_KP * 4 * NCO + THR - 1) / THR;     // dY pieces per thread
+  constexpr int XK = (PW_KP * 4 * NCIMAX + THR - 1) / THR;  // X pieces per thread (max)
   constexpr int PLMAX = NCO + NCIMAX;   // 32-channel planes per stage (max)
   constexpr int PSZ = PW_KP * 64;       // bytes per plane: 64 voxel rows of 32 H
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -929,66 +942,73 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_wgrad_kernel(PwWArgs a) {
   const bool aff = (a.prologue & VSRK_PRO_AFFINE) != 0;
   const bool do_bias = a.want_bias && ci_chunk == 0 && wave == 0;
 
-  // Per-thread chunk roles, fixed for the whole loop: dY chunk k (< NCO) and X
-  // chunk k (< ncit) are 16-byte pieces i = tid + 256k of the stage's
-  // [voxel][plane][4 x 16 B] image; every load instruction reads one tensor.
-  int dvox[NCO], dch[NCO], dlds[NCO];
+  // Per-thread chunk roles, fixed for the whole loop: dY piece k (i < 256 NCO)
+  // and X piece k (i < 256 ncit) are 16-byte pieces i = tid + THR k of the
+  // stage's [voxel][plane][4 x 16 B] image; every load instruction reads one
+  // tensor.  (Piece validity is wave-uniform: the bounds are multiples of 256.)
+  int dvox[DK], dch[DK], dlds[DK];
 #pragma unroll
-  for (int k = 0; k < NCO; ++k) {
-    const int i = tid + k * PW_THR;
+  for (int k = 0; k < DK; ++k) {
+    const int i = tid + k * THR;
     const int vox = i / (4 * NCO), within = i - vox * (4 * NCO);
     const int plane = within >> 2, q = within & 3;
     dvox[k] = vox;
     const int c = co0 + plane * 32 + q * 8;
-    dch[k] = c < a.cout ? 2 * c : -1;
-    dlds[k] = plane * PSZ + vox * 64 + q * 16;
+    dch[k] = (i < PW_KP * 4 * NCO && c < a.cout) ? 2 * c : -1;
+    dlds[k] = i < PW_KP * 4 * NCO ? plane * PSZ + vox * 64 + q * 16 : -1;
   }
-  int xvox[NCIMAX], xch[NCIMAX], xlds[NCIMAX];
+  int xvox[XK], xch[XK], xlds[XK];
   const int nxc = 4 * a.ncit;
 #pragma unroll
-  for (int k = 0; k < NCIMAX; ++k) {
-    const int i = tid + k * PW_THR;
+  for (int k = 0; k < XK; ++k) {
+    const int i = tid + k * THR;
     const int vox = i / nxc, within = i - vox * nxc;
     const int plane = within >> 2, q = within & 3;
     xvox[k] = vox;
     const int c = ci0 + plane * 32 + q * 8;
-    xch[k] = (k < a.ncit && c < a.cin) ? 2 * c : -1;
-    xlds[k] = (NCO + plane) * PSZ + vox * 64 + q * 16;
+    const bool ok = i < PW_KP * nxc;
+    xch[k] = (ok && c < a.cin) ? 2 * c : -1;
+    xlds[k] = ok ? (NCO + plane) * PSZ + vox * 64 + q * 16 : -1;
   }
 
-  uint4 ry[NCO], rx[NCIMAX];
-  auto issue = [&](int st) __attribute__((always_inline)) {
+  uint4 ry[DEPTH][DK], rx[DEPTH][XK];
+  auto issue = [&](int st, auto S) __attribute__((always_inline)) {
+    constexpr int R = decltype(S)::value;
     const int v0 = vbeg + st * PW_KP;
     const TileBase tb = tile_base(v0, a.fd);
     const Rsrc rdy = rsrc_at(aD + (int64_t)tb.n0 * a.dsn);
     const Rsrc rxx = rsrc_at(aX + (int64_t)tb.n0 * a.xsn);
 #pragma unroll
-    for (int k = 0; k < NCO; ++k) {
+    for (int k = 0; k < DK; ++k) {
       const uint32_t off = lane_off(tb, dvox[k], v0 + dvox[k], vend, a.fd, a.dsn, a.dsw);
-      ry[k] = bload16(rdy, dch[k] >= 0 ? off + dch[k] : PW_OOB);
+      ry[R][k] = bload16(rdy, dch[k] >= 0 ? off + dch[k] : PW_OOB);
     }
 #pragma unroll
-    for (int k = 0; k < NCIMAX; ++k) {
-      if (k < a.ncit) {
+    for (int k = 0; k < XK; ++k) {
+      if (xlds[k] >= 0) {
         const uint32_t off = lane_off(tb, xvox[k], v0 + xvox[k], vend, a.fd, a.xsn, a.xsw);
-        rx[k] = bload16(rxx, xch[k] >= 0 ? off + xch[k] : PW_OOB);
+        rx[R][k] = bload16(rxx, xch[k] >= 0 ? off + xch[k] : PW_OOB);
       }
     }
   };
-  auto commit = [&](int buf) __attribute__((always_inline)) {
+  auto commit = [&](int buf, auto S) __attribute__((always_inline)) {
+    constexpr int R = decltype(S)::value;
     char* base = lds + buf * (PLMAX * PSZ);
 #pragma unroll
-    for (int k = 0; k < NCO; ++k) *reinterpret_cast<uint4*>(base + dlds[k]) = ry[k];
+    for (int k = 0; k < DK; ++k)
+      if (DK * THR == PW_KP * 4 * NCO || dlds[k] >= 0) *reinterpret_cast<uint4*>(base + dlds[k]) = ry[R][k];
 #pragma unroll
-    for (int k = 0; k < NCIMAX; ++k)
-      if (k < a.ncit) *reinterpret_cast<uint4*>(base + xlds[k]) = rx[k];
+    for (int k = 0; k < XK; ++k)
+      if (xlds[k] >= 0) *reinterpret_cast<uint4*>(base + xlds[k]) = rx[R][k];
   };
+  const std::integral_constant<int, 0> I0{};
+  const std::integral_constant<int, DEPTH - 1> I1{};
 
   // prologue scale/shift of the lane's X channel in each owned block
   float psc[NCIW], psh[NCIW];
 #pragma unroll
   for (int b = 0; b < NCIW; ++b) {
-    const int c = ci0 + (wave + 4 * b) * 32 + (lane & 31);
+    const int c = ci0 + (wave + NW * b) * 32 + (lane & 31);
     const bool ok = c < a.cin;
     psc[b] = ok ? (aff ? a.pro_scale[c] : 1.f) : 0.f;
     psh[b] = ok ? (aff ? a.pro_shift[c] : 0.f) : 0.f;
@@ -1013,21 +1033,15 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_wgrad_kernel(PwWArgs a) {
   const int colb = ((g & 1) * 16 + 4 * p) * 2;
   const int rowk = 8 * (g >> 1) + q;
 
-  if (nst > 0) {
-    issue(0);
-    commit(0);
-    __syncthreads();
-  }
-  for (int st = 0; st < nst; ++st) {
-    if (st + 1 < nst) issue(st + 1);
-    const char* base = lds + (st & 1) * (PLMAX * PSZ);
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const char* base = lds + buf * (PLMAX * PSZ);
 #pragma unroll
     for (int kk = 0; kk < PW_KP / 16; ++kk) {
       const int row = kk * 16 + rowk;
       uint4 bfr[NCIW];
 #pragma unroll
       for (int b = 0; b < NCIW; ++b) {
-        const int blk = wave + 4 * b;
+        const int blk = wave + NW * b;
         if (blk < a.ncit) {
           const char* px = base + (NCO + blk) * PSZ + row * 64 + colb;
           const v4i16 x0 = ds_read_tr(px), x1 = ds_read_tr(px + 4 * 64);
@@ -1058,12 +1072,46 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_wgrad_kernel(PwWArgs a) {
         }
 #pragma unroll
         for (int b = 0; b < NCIW; ++b)
-          if (wave + 4 * b < a.ncit)
+          if (wave + NW * b < a.ncit)
             mma<H>(acc[cb][b], af, bfr[b]);
       }
     }
-    if (st + 1 < nst) commit((st + 1) & 1);
-    __syncthreads();
+  };
+
+  if constexpr (DEPTH == 1) {
+    if (nst > 0) {
+      issue(0, I0);
+      commit(0, I0);
+      __syncthreads();
+    }
+    for (int st = 0; st < nst; ++st) {
+      if (st + 1 < nst) issue(st + 1, I0);
+      compute(st & 1);
+      if (st + 1 < nst) commit((st + 1) & 1, I0);
+      __syncthreads();
+    }
+  } else {
+    // stage s lives in register set s & 1 and LDS buffer s & 1.  Issues run
+    // past the end unconditionally (every voxel out of range: zero loads, no
+    // memory traffic), so the compiler's in-order vmcnt waits stay exact.
+    if (nst > 0) {
+      issue(0, I0);
+      issue(1, I1);
+      commit(0, I0);
+      __syncthreads();
+      issue(2, I0);
+      for (int st = 0; st < nst; st += 2) {
+        compute(0);
+        commit(1, I1);  // stage st + 1
+        __syncthreads();
+        issue(st + 3, I1);
+        if (st + 1 >= nst) break;
+        compute(1);
+        commit(0, I0);  // stage st + 2
+        __syncthreads();
+        issue(st + 4, I0);
+      }
+    }
   }
 
   // slab: [co (32*NCO)][ci (32*ncit)] then dbias[32*NCO]
@@ -1074,7 +1122,7 @@ __global__ __launch_bounds__(PW_THR, 1) void pw_wgrad_kernel(PwWArgs a) {
   for (int cb = 0; cb < NCO; ++cb)
 #pragma unroll
     for (int b = 0; b < NCIW; ++b) {
-      const int blk = wave + 4 * b;
+      const int blk = wave + NW * b;
       if (blk < a.ncit) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
@@ -1607,7 +1655,7 @@ extern "C" int vsrk_conv_fwd_reduce_bnb(const vsrk_conv_desc* d, const vsrk_tens
 namespace {
 struct PwWPlan {
   bool ok;
-  int nco, ncit, ncoiw, ci_chunks, co_chunks, nchunks, nsplit, slab;
+  int nco, ncit, ncoiw, nw, ci_chunks, co_chunks, nchunks, nsplit, slab;
   int64_t vps;
   size_t ws_bytes;
 };
@@ -1640,12 +1688,20 @@ PwWPlan pw_wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk
     const char* e = getenv("VSRK_PW_WGRAD_CI8");
     ci8 = !e ? -2 : (e[0] == '1' ? 1 : 0);  // -2: automatic
   }
-  const bool one_chunk = ci8 == 1 || (ci8 == -2 && cib > 4 && std::min(cob, 8) + 4 > 10);
+  // 8-wave form (VSRK_PW_WGRAD_NW8, default on): chunks of up to 8 X blocks,
+  // one per wave, wherever the input has more than 4 blocks
+  static int nw8 = -1;
+  if (nw8 == -1) {
+    const char* e = getenv("VSRK_PW_WGRAD_NW8");
+    nw8 = !(e && e[0] == '0');
+  }
+  p.nw = (nw8 && cib > 4 && ci8 != 0) ? 8 : 4;
+  const bool one_chunk = p.nw == 8 || ci8 == 1 || (ci8 == -2 && cib > 4 && std::min(cob, 8) + 4 > 10);
   p.ncit = std::min(cib, one_chunk ? 8 : 4);
   p.ci_chunks = ceil_div(cib, p.ncit);
-  if (!one_chunk) p.ncit = ceil_div(cib, p.ci_chunks);
+  if (!one_chunk || p.nw == 8) p.ncit = ceil_div(cib, p.ci_chunks);
   if (p.nco < 2) return p;
-  p.ncoiw = ceil_div(p.ncit, 4);
+  p.ncoiw = ceil_div(p.ncit, p.nw);
   p.nchunks = p.co_chunks * p.ci_chunks;
   const int64_t nvox = (int64_t)x->n * x->d * x->h * x->w;
   if (nvox >= (1ll << 31) - 4096) return p;
@@ -1657,7 +1713,7 @@ PwWPlan pw_wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk
   }
   const int64_t steps = std::max<int64_t>(1, ceil_div64(nvox, PW_KP));
   // two workgroups per CU where the double-buffered stage fits LDS twice
-  const size_t lds = (size_t)2 * (p.nco + 4 * p.ncoiw) * PW_KP * 64;
+  const size_t lds = (size_t)2 * (p.nco + p.nw * p.ncoiw) * PW_KP * 64;
   int want = std::max(1, pw_num_cus() * (lds <= 80 * 1024 ? 2 : 1) / p.nchunks);
   if (vsrk_g_grid_cap > 0) want = std::max(1, vsrk_g_grid_cap / p.nchunks);
   want = (int)std::min<int64_t>(want, steps);
@@ -1669,12 +1725,22 @@ PwWPlan pw_wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsrk
   return p;
 }
 
-template <int NCO, int NCIW, typename H>
+// stages in flight (VSRK_PW_WGRAD_DEPTH=1|2, default 2)
+int pw_wgrad_depth() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("VSRK_PW_WGRAD_DEPTH");
+    v = (e && e[0] == '1') ? 1 : 2;
+  }
+  return v;
+}
+
+template <int NCO, int NCIW, typename H, int NW = 4>
 void launch_wgrad_pw(const PwWArgs& a, int nsplit, hipStream_t s) {
-  const size_t lds = (size_t)2 * (NCO + 4 * NCIW) * PW_KP * 64;
-  auto kern = pw_wgrad_kernel<NCO, NCIW, H>;
+  const size_t lds = (size_t)2 * (NCO + NW * NCIW) * PW_KP * 64;
+  auto kern = pw_wgrad_depth() == 2 ? pw_wgrad_kernel<NCO, NCIW, H, 2, NW> : pw_wgrad_kernel<NCO, NCIW, H, 1, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  kern<<<dim3(nsplit, a.nchunks), PW_THR, lds, s>>>(a);
+  kern<<<dim3(nsplit, a.nchunks), NW * 64, lds, s>>>(a);
 }
 }  // namespace
 
@@ -1715,13 +1781,14 @@ int vsrk_conv_wgrad_pw(const vsrk_conv_desc* d, const vsrk_tensor5* x, const vsr
   a.slab = p.slab;
   a.want_bias = dbias != nullptr;
   if (a.nvox > 0) {
-    const bool w2 = p.ncoiw == 2;
+    const bool w2 = p.ncoiw == 2, nw8 = p.nw == 8;
     switch (p.nco) {
 #define PWW_CASE(N)                                                                   \
   case N:                                                                             \
     vsrk_dispatch16(x->dtype, [&](auto tag) {                                       \
       using H = decltype(tag);                                                      \
-      if (w2) launch_wgrad_pw<N, 2, H>(a, p.nsplit, s);                            \
+      if (nw8) launch_wgrad_pw<N, 1, H, 8>(a, p.nsplit, s);                        \
+      else if (w2) launch_wgrad_pw<N, 2, H>(a, p.nsplit, s);                       \
       else launch_wgrad_pw<N, 1, H>(a, p.nsplit, s);                               \
       return 0;                                                                     \
     });                                                                             \
