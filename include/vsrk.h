@@ -168,7 +168,9 @@ int vsrk_conv_set_algo(int32_t mode);
  * default on), "wgrad_pipe" (pipelined 16-bit 3x3(x3) weight gradient, default
  * on), "wgrad_roll" (rolling-depth Conv3d 3x3x3 weight gradient), "wgrad_row"
  * (rolling-row Conv2d 3x3 weight gradient over 64 x 64 channel blocks,
- * default on); mode -1 = default/environment (VSRK_CONV_FAST, VSRK_CONV_PW,
+ * default on), "roll_fold" (the depth-folded rolling forward of a Conv3d
+ * 3x3x3 with one output depth from three slices, duf_net.py:214, default on;
+ * env VSRK_ROLL_FOLD); mode -1 = default/environment (VSRK_CONV_FAST, VSRK_CONV_PW,
  * VSRK_CONV_ROLL, VSRK_CONV_THIN, VSRK_WGRAD_PIPE, VSRK_WGRAD_ROLL,
  * VSRK_WGRAD_ROW), 0 = off, 1 = on where eligible.  Every path computes the
  * same result as the generic kernels within bf16 rounding. */

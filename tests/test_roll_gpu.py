@@ -460,3 +460,33 @@ def test_roll_2d_resident_weights_forced(case, epi):
     ulp = torch.maximum(y0.abs(), y2.abs()) * 2.0 ** -7 + 2.0 ** -18 * ref.abs().max().item()
     assert (d <= ulp).all(), float((d / ulp).max())
     assert int((d > 0).sum()) <= 1e-3 * d.numel(), int((d > 0).sum())
+
+
+FOLD_CASES = [
+    # (N, D=3, H, W, Cin, Cout, depth pad 0, channel offset): one output depth
+    (1, 3, 16, 32, 224, 32, 0, 0),    # DUF's last unit (F = 224), one 32-row tile
+    (2, 3, 40, 70, 48, 64, 0, 8),     # partial row / column tiles, two output blocks, sliced input
+    (1, 3, 33, 32, 16, 32, 0, 0),     # one chunk per depth tap, a 1-row second tile
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", FOLD_CASES)
+def test_roll_depth_fold(case, dtype):
+    """the depth-folded form (conv_roll_fold.hip: 3 slices -> 1 output depth
+    as a 3x3 conv over (kd, channel) chunks, 32-row tiles) against fp64 with
+    and without the BN prologue, bitwise invariant under the grid cap, and
+    bitwise equal to the 3-D rolling form it replaces (both accumulate an
+    output voxel slice by slice, chunk by chunk, tap by tap)"""
+    for prologue in (False, True):
+        y, ref = _run(case, dtype, prologue)
+        assert (y - ref).abs().max().item() <= _tol(dtype, ref)
+        for cap in (1, 3):
+            yc, _ = _run(case, dtype, prologue, cap=cap)
+            assert torch.equal(yc, y), cap
+    F.set_conv_path("roll_fold", 0)
+    try:
+        y3, _ = _run(case, dtype, True)
+    finally:
+        F.set_conv_path("roll_fold", -1)
+    assert torch.equal(y3, y), (y3 - y).abs().max().item()

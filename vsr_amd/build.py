@@ -23,7 +23,8 @@ FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-re
 # operand pair to marshal the packed registers (76 -> 28 v_mov per weight-
 # gradient stage), and packed f32 VALU beside MFMAs costs more issue than the
 # scalar form (MI355X_MICROARCH.md, cycle constants).
-SRC_FLAGS = {"conv_roll.hip": ["-fno-slp-vectorize"], "conv_wgrad_roll.hip": ["-fno-slp-vectorize"]}
+SRC_FLAGS = {"conv_roll.hip": ["-fno-slp-vectorize"], "conv_roll_fold.hip": ["-fno-slp-vectorize"],
+             "conv_wgrad_roll.hip": ["-fno-slp-vectorize"]}
 
 
 def sources() -> list[Path]:

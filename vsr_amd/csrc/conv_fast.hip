@@ -52,9 +52,10 @@ extern "C" int vsrk_conv_set_path(const char* path, int32_t mode) {
   else if (p == "wgrad_roll") vsrk_conv_set_wgrad_roll_mode(mode);
   else if (p == "wgrad_row") vsrk_conv_set_wgrad_row_mode(mode);
   else if (p == "roll_wr") vsrk_conv_set_roll_wr_mode(mode);
+  else if (p == "roll_fold") vsrk_conv_set_roll_fold_mode(mode);
   else if (p == "stencil") vsrk_conv_set_stencil_mode(mode);
   else if (p == "pw_wide") g_pw_wide_mode = mode;
-  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, pw, roll, roll_wr, thin, wgrad_pipe, wgrad_roll, wgrad_row, stencil)",
+  else VSRK_CHECK(false, "conv_set_path: unknown path '%s' (fast, pw, roll, roll_wr, roll_fold, thin, wgrad_pipe, wgrad_roll, wgrad_row, stencil)",
                   path);
   return VSRK_OK;
 }

@@ -103,7 +103,8 @@ constexpr int RNSLOT = 3;
 // 32 -> F: 47 -> 20).
 template <int KD, int NT, int WR = 0>
 struct RollGeo {
-  static_assert((KD == 3 && NT == 1) || (KD == 1 && NT == 2), "rolling conv forms: 3x3x3 / 32 or 3x3 / 64");
+  static_assert((KD == 3 && NT == 1) || (KD == 1 && (NT == 2 || NT == 1)),
+                "rolling conv forms: 3x3x3 / 32, 3x3 / 64 or (folded depth) 3x3 / 32");
   static constexpr int NB = 9 * KD * NT;           // B pieces: 27 / 18
   static constexpr int NI = WR ? RNAI : RNAI + NB;  // 47 / 38 (WR: 20)
   static constexpr int NQ = (NI + RNW - 1) / RNW;  // pieces per wave and stage: 6 / 5 (WR: 3)
@@ -137,8 +138,13 @@ struct RollGeo {
 // (the per-tile partials hold sum dy' (bnx - mean); the final kernel scales
 // by invstd)
 enum { RE_RES = 1, RE_MASK = 2, RE_ACC = 4, RE_RELU = 8, RE_PRELU = 16, RE_PMASK = 32, RE_BNRED = 64 };
-// sub-pixel operand (2-D forms): none, input view, output view
-enum { SP_NONE = 0, SP_X = 1, SP_Y = 2 };
+// sub-pixel operand (2-D forms): none, input view, output view.  SP_FOLD:
+// the depth-folded form of a Conv3d 3x3x3 with one output depth from three
+// input slices (DUF's last unit, padding (0, 1, 1), duf_net.py:214): a 3x3
+// conv over the (kd, channel) chunks of the three slices -- chunk i reads
+// slice kd = sptap[i] at element offset spoff[i] and the weights of depth tap
+// kd (fold_wstride elements apart in the packed [kd][kh][kw][co][ci] image)
+enum { SP_NONE = 0, SP_X = 1, SP_Y = 2, SP_FOLD = 3 };
 constexpr int RMAXSUB = 64;  // chunk / block table entries (1024 logical channels)
 
 // Division by a launch constant d (dividends < 2^31): q = (x * mul) >> p with
@@ -179,6 +185,10 @@ struct RollArgs {
   // row / column + physical channel) and its tap mask (bit kh*3 + kw)
   const float* act_param;
   int prio;  // A/B knob (VSRK_ROLL_PRIO=1): s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD)
+  // SP_FOLD: input chunks per depth tap, element stride of a depth tap in the
+  // packed weights, logical channels of the prologue tables (3 x cin; their
+  // constants repeat every cin)
+  int fold_nc, fold_wstride, fold_tab, fold_cin;
   const float* mask_slope;  // RE_PMASK: the PReLU slope a (device scalar)
   double* slope_part;       // RE_PMASK: [block][wave] partials of the slope gradient
   // RE_BNRED: the BN input (y's geometry and strides), its per-channel
@@ -232,9 +242,22 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
   if (a.prio && wave >= 4) __builtin_amdgcn_s_setprio(1);
   char* wres = lds + RNSLOT * RSLOT;  // WR: [chunk][B piece] 1 KB pieces of the resident output block
   float* lbias = reinterpret_cast<float*>(wres + (WR ? a.nchunk * G::NB * 1024 : 0));  // [cout_pad] bias * out_scale
+  // (SP_FOLD: the tables span the fold's 3 x cin logical channels)
+  const int tabc = SP == SP_FOLD ? a.fold_tab : a.cin_pad;
   float* lsc = lbias + a.cout_pad;                                // [cin_pad] prologue scale / shift
-  float* lsh = lsc + a.cin_pad;
-  if constexpr (PRO) stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, a.cin_pad, tid, RNW * 64);
+  float* lsh = lsc + tabc;
+  if constexpr (PRO) {
+    if constexpr (SP == SP_FOLD) {
+      for (int i = tid; i < tabc; i += RNW * 64) {
+        const int c = i % a.fold_cin;
+        const bool aff = (a.prologue & VSRK_PRO_AFFINE) != 0;
+        lsc[i] = aff ? a.pro_scale[c] : 1.f;
+        lsh[i] = aff ? a.pro_shift[c] : 0.f;
+      }
+    } else {
+      stage_prologue(lsc, lsh, a.prologue, a.pro_scale, a.pro_shift, a.cin, a.cin_pad, tid, RNW * 64);
+    }
+  }
   for (int i = tid; i < a.cout_pad; i += RNW * 64) {
     float b = 0.f;
     if (a.bias && i < a.cout) {
@@ -249,7 +272,7 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
     lbias[i] = b * a.out_scale;
   }
   // RE_BNRED: [4][cout_pad] BN constants after the prologue tables
-  float* lbn = lbias + a.cout_pad + 2 * a.cin_pad;
+  float* lbn = lbias + a.cout_pad + 2 * tabc;
   if constexpr ((EM & RE_BNRED) != 0) {
     for (int i = tid; i < a.cout_pad; i += RNW * 64) {
       const bool ok = i < a.cout;
@@ -396,8 +419,13 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
     Dma d;
     const int di = k.tl.di_lo + k.sl;
     const int c0 = k.c * RCH;
-    d.xb = reinterpret_cast<const H*>(a.x.ptr) + (k.tl.xo + di * a.x.sd + (SP == SP_X ? a.spoff[k.c] : c0));
-    d.wsrc = reinterpret_cast<const H*>(a.w) + (k.tl.n0 * a.cin_pad + c0);
+    d.xb = reinterpret_cast<const H*>(a.x.ptr) + (k.tl.xo + di * a.x.sd + (SP == SP_X || SP == SP_FOLD ? a.spoff[k.c] : c0));
+    if constexpr (SP == SP_FOLD) {
+      const int kdf = a.sptap[k.c];
+      d.wsrc = reinterpret_cast<const H*>(a.w) + (k.tl.n0 * a.cin_pad + kdf * a.fold_wstride + (k.c - kdf * a.fold_nc) * RCH);
+    } else {
+      d.wsrc = reinterpret_cast<const H*>(a.w) + (k.tl.n0 * a.cin_pad + c0);
+    }
     const unsigned km = kd_mask(k.tl.z0, k.tl.z1, di);
     d.use = (k.m & qa) | ((km & 1) ? qkd0 : 0u) | ((km & 2) ? qkd1 : 0u) | ((km & 4) ? qkd2 : 0u);
     return d;
@@ -432,7 +460,7 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
         const int c = p / G::NB, bp = p - c * G::NB;
         const int tap = bp / NT, nt = bp - tap * NT;
         const H* src = reinterpret_cast<const H*>(a.w) + ((tap * a.cout_pad + n0 + nt * 32 + co) * a.cin_pad + c * RCH + 8 * ph);
-        glds16_m0(src, lds_addr(wres) + p * 1024);
+        glds16_m0(src, __builtin_amdgcn_readfirstlane(lds_addr(wres) + p * 1024));
       }
       wblk = n0;
     }
@@ -575,7 +603,7 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
         const unsigned tkb = b == 0 ? tk0 : tk1;  // sub-pixel forms: taps of this set's phase
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh) {
-          if (SP == SP_NONE || ((tkb >> (kh * 3 + kw)) & 1)) {
+          if ((SP != SP_X && SP != SP_Y) || ((tkb >> (kh * 3 + kw)) & 1)) {
 #pragma unroll
             for (int ms = 0; ms < RMS; ++ms)
               if constexpr (!(ROLL_ABL & 1)) mma<H>(acc[b][ms], bw[g & 1][kh], ax[kw & 1][ms + kh]);
@@ -1092,6 +1120,98 @@ int launch_roll(const RollArgs& a, size_t lds, int grid, hipStream_t s) {
 
 }  // namespace
 
+#ifdef ROLL_FOLD_TU
+// The depth-folded forward (this translation unit is conv_roll_fold.hip:
+// ROLL_RMS 4, 32-row tiles).  DUF's last unit is Conv3d(224, 32, 3, padding
+// (0, 1, 1)) over three input slices into one output depth (duf_net.py:214):
+// a rolling walk finds one kd tap per staged slice, so its stage carried a
+// third of the 3-D form's MFMAs beside the same 47 DMA pieces (and 27 B
+// fragment reads) -- it ran on conv_fast at ~0.22 of peak.  Folded, it is a
+// 3x3 conv over 3 x cin (kd, channel) chunks with one 32-channel output
+// block: a stage stages 37 A pieces (34 x 34 halo voxels of 16 channels) and
+// the 9 B pieces of its depth tap, and each wave runs 9 taps x 4 rows = 36
+// MFMAs per stage (18 in the 3-D form's one-bank stages).
+// 1 = launched, 0 = not eligible, < 0 = -(error status)
+int vsrk_conv_fwd_roll_fold(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                            const float* pro_scale, const float* pro_shift, const vsrk_tensor5* y, hipStream_t s) {
+  if (d->kd != 3 || d->kh != 3 || d->kw != 3 || d->pd != 0 || x->d != 3 || y->d != 1) return 0;
+  if (!vsrk_is16(x->dtype) || y->dtype != x->dtype || x->shuffle > 1 || y->shuffle > 1) return 0;
+  if (d->act != VSRK_ACT_NONE && d->act != VSRK_ACT_RELU) return 0;
+  if (d->accumulate || d->mask_slope || d->bias_perm_r > 1) return 0;
+  if (x->c % RCH != 0 || 3 * (x->c / RCH) > RMAXSUB || !chunk_ok(x, 2)) return 0;
+  if (y->c % 32 != 0 || ((uintptr_t)y->ptr) % 16 != 0 || y->sn % 8 || y->sh % 8 || y->sw % 8) return 0;
+  if (d->ph < 0 || d->ph > 2 || d->pw < 0 || d->pw > 2) return 0;
+  if (y->h != x->h + 2 * d->ph - 2 || y->w != x->w + 2 * d->pw - 2 || y->n != x->n) return 0;
+  for (const vsrk_tensor5* t : {x, y}) {  // every element offset fits in 32 bits
+    const int64_t span = (int64_t)(t->n - 1) * t->sn + (int64_t)(t->d - 1) * t->sd +
+                         (int64_t)(t->h + RFTH + 2) * t->sh + (int64_t)(t->w + 2 * RHW) * t->sw + t->c;
+    if (span >= (1ll << 31) || t->sn < 0 || t->sd < 0 || t->sh < 0 || t->sw < 0) return 0;
+  }
+  RollArgs a;
+  a.x.ptr = (char*)x->ptr;
+  a.x.d = 1; a.x.h = x->h; a.x.w = x->w;
+  a.x.sn = (int)x->sn; a.x.sd = (int)x->sd; a.x.sh = (int)x->sh; a.x.sw = (int)x->sw;
+  a.y.ptr = (char*)y->ptr;
+  a.y.d = 1; a.y.h = y->h; a.y.w = y->w;
+  a.y.sn = (int)y->sn; a.y.sd = (int)y->sd; a.y.sh = (int)y->sh; a.y.sw = (int)y->sw;
+  a.res = a.y;
+  a.msk = a.y;
+  a.w = w_packed;
+  a.bias = bias;
+  a.bias_r = 1;
+  a.pro_scale = pro_scale;
+  a.pro_shift = pro_shift;
+  a.cin = 3 * x->c;
+  a.cout = y->c;
+  a.cin_pad = round_up(x->c, 32);  // of the packed weights
+  a.cout_pad = round_up(y->c, 128);
+  a.pd = 0;
+  a.ph = d->ph;
+  a.pw = d->pw;
+  a.prologue = d->prologue;
+  a.out_scale = d->out_scale;
+  const int nc = x->c / RCH;
+  a.nchunk = 3 * nc;
+  a.fold_nc = nc;
+  a.fold_wstride = 9 * a.cout_pad * a.cin_pad;
+  a.fold_tab = 3 * x->c;
+  a.fold_cin = x->c;
+  a.act_param = nullptr;
+  a.prio = 0;
+  a.mask_slope = nullptr;
+  a.slope_part = nullptr;
+  for (int i = 0; i < a.nchunk; ++i) {
+    const int kd = i / nc;
+    a.spoff[i] = (int)(kd * x->sd + (i - kd * nc) * RCH);
+    a.sptap[i] = (uint16_t)kd;
+  }
+  const int tiles_h = ceil_div(y->h, RFTH), tiles_w = ceil_div(y->w, TW), ntn = ceil_div(y->c, 32);
+  const int64_t ntiles = (int64_t)y->n * tiles_h * tiles_w * ntn;
+  if (ntiles == 0) return 1;
+  VSRK_CHECK(ntiles < (1ll << 31), "conv_fwd(roll fold): too many tiles");
+  a.dzc = 1;
+  a.ntn = make_rdiv(ntn);
+  a.nzc = make_rdiv(1);
+  a.tiles_w = make_rdiv(tiles_w);
+  a.tiles_h = make_rdiv(tiles_h);
+  a.ntiles = (int)ntiles;
+  using G = RollGeo<1, 1>;
+  const size_t tables = (size_t)a.cout_pad * 4 + (d->prologue ? 2 * (size_t)a.fold_tab * 4 : 0);
+  const size_t lds = (size_t)RNSLOT * G::SLOT + tables;
+  if (lds > 160 * 1024) return 0;
+  const int grid = (int)vsrk_capped_grid(std::min<int64_t>(ntiles, roll_num_cus()));
+  const bool relu = d->act == VSRK_ACT_RELU;
+  int rc = vsrk_dispatch16(x->dtype, [&](auto tag) {
+    using H = decltype(tag);
+    if (d->prologue)
+      return relu ? launch_roll<1, 1, 1, RE_RELU, SP_FOLD, H>(a, lds, grid, s) : launch_roll<1, 1, 1, 0, SP_FOLD, H>(a, lds, grid, s);
+    return relu ? launch_roll<1, 1, 0, RE_RELU, SP_FOLD, H>(a, lds, grid, s) : launch_roll<1, 1, 0, 0, SP_FOLD, H>(a, lds, grid, s);
+  });
+  if (rc == VSRK_ERR_UNSUPPORTED) return 0;
+  return rc == VSRK_OK ? 1 : -rc;
+}
+#else  // ROLL_FOLD_TU
+
 // > 0: output depths per tile of both rolling kernels (test knob), 0: automatic
 int vsrk_g_roll_dz = 0;
 
@@ -1105,6 +1225,11 @@ void vsrk_conv_set_roll_wr_mode(int mode) { g_roll_wr_mode = mode; }
 
 void vsrk_conv_set_roll_mode(int mode) { g_roll_mode = mode; }
 
+// the depth-folded form for one output depth from three slices: -1 from
+// VSRK_ROLL_FOLD (unset: on), 0 off, 1 on
+int g_roll_fold_mode = -1;
+void vsrk_conv_set_roll_fold_mode(int mode) { g_roll_fold_mode = mode; }
+
 // 1 = launched, 0 = not eligible, < 0 = -(error status)
 size_t vsrk_roll_slope_ws_bytes() { return (size_t)roll_num_cus() * RNW * sizeof(double); }
 
@@ -1115,6 +1240,10 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   if (g_roll_mode < 0) {
     const char* e = getenv("VSRK_CONV_ROLL");
     g_roll_mode = !e ? 2 : (e[0] == '0' ? 0 : 1);
+  }
+  if (g_roll_fold_mode < 0) {
+    const char* e = getenv("VSRK_ROLL_FOLD");
+    g_roll_fold_mode = (e && e[0] == '0') ? 0 : 1;
   }
   if (g_roll_mode == 0) return 0;
   if (!vsrk_is16(x->dtype) || y->dtype != x->dtype) return 0;
@@ -1138,6 +1267,11 @@ int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const voi
   }
   if (d->act == VSRK_ACT_PRELU && (k3 || !d->act_param)) return 0;
   if (k3 && (residual || mask || d->accumulate)) return 0;
+  // a single output depth from three slices (DUF's last unit): the depth-
+  // folded 2-D form (conv_roll_fold.hip)
+  if (k3 && y->d == 1 && x->d == 3 && d->pd == 0 && !bnred && !residual && !mask && !pmask && g_roll_fold_mode != 0) {
+    if (const int rf = vsrk_conv_fwd_roll_fold(d, x, w_packed, bias, pro_scale, pro_shift, y, s)) return rf;
+  }
   // automatic mode: a single output depth has no slice reuse to roll over;
   // the per-kd-stage kernel is faster there (DUF's last unit, 3 -> 1 slices
   // at F = 224: 817 vs 943 us, r3p microbench)
@@ -1419,3 +1553,4 @@ int vsrk_roll_bnred_final(const vsrk_roll_bnred& r, int cout, float* sum_dy, flo
 size_t vsrk_roll_bnred_ws_floats(const vsrk_tensor5* y) {  // every depth its own tile run (an upper bound)
   return (size_t)y->n * ceil_div(y->h, RFTH) * ceil_div(y->w, TW) * ceil_div(y->c, 32) * std::max(y->d, 1) * RNW * 64;
 }
+#endif  // ROLL_FOLD_TU

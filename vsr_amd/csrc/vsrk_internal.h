@@ -64,6 +64,11 @@ size_t vsrk_roll_bnred_ws_floats(const vsrk_tensor5* y);
 size_t vsrk_roll_slope_ws_bytes();
 void vsrk_conv_set_roll_mode(int mode);
 void vsrk_conv_set_roll_wr_mode(int mode);
+void vsrk_conv_set_roll_fold_mode(int mode);
+// the depth-folded rolling forward (conv_roll_fold.hip): one output depth from
+// three slices; 1 launched, 0 not eligible, < 0 -(error status)
+int vsrk_conv_fwd_roll_fold(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                            const float* pro_scale, const float* pro_shift, const vsrk_tensor5* y, hipStream_t s);
 
 // pointwise (1x1x1) bf16 conv (conv_pw.hip): forward / data gradient and
 // weight gradient; same return convention (the wgrad launches its own reduce)

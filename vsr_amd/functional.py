@@ -397,8 +397,8 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, k, pad, dw: torch.Tensor, dbia
 
 
 def set_conv_path(path: str, mode: int) -> None:
-    """Select a conv kernel family ("fast", "pw", "pw_wide", "roll", "roll_wr", "thin", "wgrad_pipe", "wgrad_roll",
-    "wgrad_row"):
+    """Select a conv kernel family ("fast", "pw", "pw_wide", "roll", "roll_wr", "roll_fold", "thin", "wgrad_pipe",
+    "wgrad_roll", "wgrad_row"):
     -1 default, 0 off, 1 on
     (for "roll" / "wgrad_roll": 1 forces the rolling kernel on every eligible
     shape, the default also skips shallow output depths where it is slower;

@@ -46,6 +46,7 @@ class BaseNet(nn.Module):
         self.overlap_wgrad = self._OVERLAP_WGRAD if env is None else env != "0"
         self._side = None
         self._side_used = False
+        self._side_keep: list = []  # operands of side-stream launches captured into a graph (see _on_wgrad_stream)
         self._packers: dict = {}
 
     # -- gradient plumbing used by the subclasses' backward passes ----------
@@ -86,6 +87,13 @@ class BaseNet(nn.Module):
             out = fn()
         for t in reads:
             t.record_stream(self._side)
+        if torch.cuda.is_current_stream_capturing():
+            # record_stream does not defer a free inside graph capture: a
+            # tensor dropped now could go to a later captured allocation on
+            # the main stream while the side stream still reads it.  Hold
+            # every operand until _join_wgrad orders the main stream after
+            # the side stream.
+            self._side_keep.extend(reads)
         self._side_used = True
         return out
 
@@ -106,6 +114,7 @@ class BaseNet(nn.Module):
         if self._side_used:
             torch.cuda.current_stream().wait_stream(self._side)
             self._side_used = False
+        self._side_keep.clear()
 
     def set_precision(self, precision: str, loss_scale: float | None = None) -> "BaseNet":
         """'bf16' or 'fp16' (16-bit activations and data gradients, fp32 master
