@@ -46,6 +46,30 @@
 #define ROLL_NT 0  // A/B: non-temporal output stores in the transposed epilogue
 #endif
 typedef uint32_t roll_u32x4 __attribute__((ext_vector_type(4)));
+typedef int roll_v4i __attribute__((ext_vector_type(4)));
+// Raw buffer resource over [base, base + 2 GiB) (wave-uniform base): offsets
+// at or beyond 0x7FFFFFF0 read as zero and drop stores -- the register-
+// transposed epilogue's out-of-range voxels without branches
+typedef __amdgpu_buffer_rsrc_t RRsrc;
+constexpr uint32_t ROLL_OOB = 0x80000000u;
+__device__ __forceinline__ RRsrc roll_rsrc(const void* base) {
+  const uint64_t b = (uint64_t)base;
+  const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)u, 0, 0x7FFFFFF0, 0x00020000);
+}
+__device__ __forceinline__ uint4 roll_bload16(RRsrc r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+// SWAP (2-D forms without a prefetched operand): the flush transposes the
+// accumulators in registers (epilogue_sw) instead of parking them in LDS;
+// measured on the EDSR 64 -> 64 body (profiles/r6_roll_defer_ab.txt, nodefer):
+// plain forward -13 %, data gradient -7 %, ReLU forward -5 %, while the
+// prefetched-operand 2-D forms and the 3-D forms lost 3-4 % with it and keep
+// the LDS park (0 builds the park everywhere)
+#ifndef ROLL_SWAP
+#define ROLL_SWAP 1
+#endif
 
 namespace {
 using namespace vsrk_conv;
@@ -236,6 +260,7 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
   // (3-D: the BN input of RE_BNRED, read by the flush of the slice's finished depth)
   constexpr bool PREF = (KD == 1 && ((EM & RE_RES) != 0) != ((EM & RE_MASK) != 0) && !(EM & RE_ACC)) ||
                         (KD == 3 && (EM & RE_BNRED) != 0);
+  constexpr bool SWAP = ROLL_SWAP && KD == 1 && !PREF;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -795,6 +820,110 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
       }
     }
   };
+  // Register-transposed epilogue (SWAP: 2-D, no prefetched operand; output
+  // block nt of depth dz).  The 32x32 accumulator of a row holds, in lane
+  // (r, hf), voxel r and the channels 8 g + 4 hf + i (register 4 g + i).
+  // v_permlane32_swap on the register pairs (4 g + i, 4 g + 4 + i), g = 0, 2,
+  // leaves lane (r, hf) with the 8 consecutive channels 16 p + 8 hf .. +7 of
+  // voxel r in registers 8 p .. +7; v_permlane16_swap on the pairs (e, 8 + e)
+  // then trades the upper 16 lanes' p = 0 chunk for the lower 16 lanes' p = 1
+  // chunk: lane (r, hf) ends with the 8-channel chunk ecc = 2 (r >> 4) + hf of
+  // the two voxels (r & 15) + 16 q in registers 8 q .. +7.  Every global
+  // access is 16 contiguous bytes (a wave instruction covers 16 whole 64-byte
+  // voxel rows), as in epilogue_tr, without the LDS park and its waits; the
+  // out-of-range voxels take a buffer offset past the resource (loads read
+  // zero, stores are dropped).
+  const int ecc = 2 * (r >> 4) + hf;
+  auto epilogue_sw = [&](const f32x16 (&A)[RMS], const RTile& tl, int dz, int nt) __attribute__((always_inline)) {
+    const int64_t sbase = (int64_t)tl.nb * a.y.sn + (int64_t)dz * a.y.sd;
+    const RRsrc ry = roll_rsrc(reinterpret_cast<const H*>(a.y.ptr) + sbase);
+    // (RE_PMASK: the mask has y's geometry and strides, the host checks)
+    const RRsrc rpm = roll_rsrc(reinterpret_cast<const H*>((EM & RE_PMASK) ? a.msk.ptr : a.y.ptr) + sbase);
+    const RRsrc rmk = roll_rsrc(reinterpret_cast<const H*>(a.msk.ptr) + ((int64_t)tl.nb * a.msk.sn + (int64_t)dz * a.msk.sd));
+    const RRsrc rrs = roll_rsrc(reinterpret_cast<const H*>(a.res.ptr) + ((int64_t)tl.nb * a.res.sn + (int64_t)dz * a.res.sd));
+    const int co = tl.n0 + nt * 32 + 8 * ecc;
+    const int ych = (SP == SP_Y ? a.spoff[(tl.n0 >> 5) + nt] : tl.n0 + nt * 32) + 8 * ecc;
+    float bsv[8];
+    {
+      const float4 b0 = *reinterpret_cast<const float4*>(lbias + co);
+      const float4 b1 = *reinterpret_cast<const float4*>(lbias + co + 4);
+      bsv[0] = b0.x; bsv[1] = b0.y; bsv[2] = b0.z; bsv[3] = b0.w;
+      bsv[4] = b1.x; bsv[5] = b1.y; bsv[6] = b1.z; bsv[7] = b1.w;
+    }
+#pragma unroll
+    for (int ms = 0; ms < RMS; ++ms) {
+      const int ho = tl.h0 + wave * RMS + ms;
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = A[ms][i];
+#pragma unroll
+      for (int g = 0; g < 4; g += 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, v[4 * g + i]),
+                                                           __builtin_bit_cast(uint32_t, v[4 * g + 4 + i]), false, false);
+          v[4 * g + i] = __builtin_bit_cast(float, (uint32_t)sw[0]);
+          v[4 * g + 4 + i] = __builtin_bit_cast(float, (uint32_t)sw[1]);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, v[e]),
+                                                         __builtin_bit_cast(uint32_t, v[8 + e]), false, false);
+        v[e] = __builtin_bit_cast(float, (uint32_t)sw[0]);
+        v[8 + e] = __builtin_bit_cast(float, (uint32_t)sw[1]);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {  // the voxel (r & 15) + 16 q
+        const int wo = tl.w0 + (r & 15) + 16 * q;
+        const bool ok = ho < a.y.h && wo < a.y.w;
+        const uint32_t yoff = ok ? 2u * (uint32_t)(ho * a.y.sh + wo * a.y.sw + ych) : ROLL_OOB;
+        float t[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          t[e] = fmaf(v[8 * q + e], osc, bsv[e]);
+          if constexpr (EM & RE_RELU) t[e] = fmaxf(t[e], 0.f);
+          if constexpr (EM & RE_PRELU) t[e] = t[e] > 0.f ? t[e] : pslope * t[e];
+        }
+        if constexpr (EM & RE_MASK) {
+          float m[8];
+          Chunk<H>::unpack(roll_bload16(rmk, ok ? 2u * (uint32_t)(ho * a.msk.sh + wo * a.msk.sw + co) : ROLL_OOB), m);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t[e] = m[e] > 0.f ? t[e] : 0.f;
+        }
+        if constexpr (EM & RE_PMASK) {
+          if constexpr (EM & RE_ACC) {  // the consumer's PReLU backward sees the whole sum: after the accumulate
+            float o[8];
+            Chunk<H>::unpack(roll_bload16(ry, yoff), o);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) t[e] += o[e];
+          }
+          float m[8];
+          Chunk<H>::unpack(roll_bload16(rpm, yoff), m);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t[e] = m[e] > 0.f ? t[e] : mslope * t[e];
+          float tr[8];
+          Chunk<H>::unpack(Chunk<H>::pack(t), tr);  // the stored (rounded) values, as prelu_bwd reads them
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (m[e] < 0.f) sacc = fmaf(tr[e], m[e], sacc);  // (m = 0 off the image)
+        }
+        if constexpr (EM & RE_RES) {
+          float rr[8];
+          Chunk<H>::unpack(roll_bload16(rrs, ok ? 2u * (uint32_t)(ho * a.res.sh + wo * a.res.sw + co) : ROLL_OOB), rr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t[e] += rr[e];
+        }
+        if constexpr ((EM & RE_ACC) && !(EM & RE_PMASK)) {
+          float o[8];
+          Chunk<H>::unpack(roll_bload16(ry, yoff), o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t[e] += o[e];
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(roll_v4i, Chunk<H>::pack(t)), ry, (int)yoff, 0, 0);
+      }
+    }
+  };
   // Flush after slice pdi of tile tl.  KD 3: the banks whose output depth
   // takes no more contributions -- dz = pdi + pd - 2 when the walk stays in
   // the tile (all = false), every bank at the end of the tile -- are stored
@@ -843,7 +972,10 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
     } else {
 #pragma unroll
       for (int b = 0; b < NACC; ++b) {
-        if (!(ROLL_ABL & 4) && P >= tl.z0 && P < tl.z1) epilogue_tr(acc[b], tl, P, b, use_pre ? EO_PRE : EO_LOAD, scr);
+        if (!(ROLL_ABL & 4) && P >= tl.z0 && P < tl.z1) {
+          if constexpr (SWAP) epilogue_sw(acc[b], tl, P, b);
+          else epilogue_tr(acc[b], tl, P, b, use_pre ? EO_PRE : EO_LOAD, scr);
+        }
 #pragma unroll
         for (int m = 0; m < RMS; ++m)
 #pragma unroll
