@@ -70,6 +70,12 @@ __device__ __forceinline__ uint4 roll_bload16(RRsrc r, uint32_t off) {
 #ifndef ROLL_SWAP
 #define ROLL_SWAP 1
 #endif
+// PREF2D: the residual / mask operand of a 2-D tile prefetched into
+// registers during the slice's last stages (0: loaded in the flush, which
+// then takes the SWAP form)
+#ifndef ROLL_PREF2D
+#define ROLL_PREF2D 1
+#endif
 
 namespace {
 using namespace vsrk_conv;
@@ -258,7 +264,7 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
   // the residual / mask operand of a 2-D tile is loaded into registers during
   // its last stage (one extra operand, no accumulate)
   // (3-D: the BN input of RE_BNRED, read by the flush of the slice's finished depth)
-  constexpr bool PREF = (KD == 1 && ((EM & RE_RES) != 0) != ((EM & RE_MASK) != 0) && !(EM & RE_ACC)) ||
+  constexpr bool PREF = (ROLL_PREF2D && KD == 1 && ((EM & RE_RES) != 0) != ((EM & RE_MASK) != 0) && !(EM & RE_ACC)) ||
                         (KD == 3 && (EM & RE_BNRED) != 0);
   constexpr bool SWAP = ROLL_SWAP && KD == 1 && !PREF;
   extern __shared__ __attribute__((aligned(16))) char lds[];
