@@ -149,7 +149,8 @@ int vsrk_conv_fwd_reduce(const vsrk_conv_desc* desc, const vsrk_tensor5* x, cons
  * kernel's (1x1, no bias); VSRK_ERR_UNSUPPORTED otherwise (the caller runs
  * vsrk_conv_fwd + vsrk_prelu_bwd).  Fixed-order per-wave partials and a
  * fixed-order final sum (deterministic); workspace
- * vsrk_conv_prelu_bwd_workspace() bytes. */
+ * vsrk_conv_prelu_bwd_workspace() bytes.  da == NULL defers the slope
+ * gradient: the partials stay in the workspace (see vsrk_slope_final_sum). */
 size_t vsrk_conv_prelu_bwd_workspace(void);
 int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* desc, const vsrk_tensor5* x, const void* w_packed,
                             const float* bias, const vsrk_tensor5* y_fwd, const vsrk_tensor5* y, int32_t c_lo,
@@ -249,6 +250,19 @@ int vsrk_prelu_bwd(const vsrk_tensor5* y, const vsrk_tensor5* dy, const vsrk_ten
 int vsrk_prelu_bwd_pre(const vsrk_tensor5* x, const vsrk_tensor5* dy, const vsrk_tensor5* dy2, const float* a,
                        const vsrk_tensor5* dx, float* da, int32_t accumulate_da, void* workspace,
                        size_t workspace_bytes, void* stream);
+
+/* Deferred PReLU slope gradients (DRF: 12 PReLUs x 30 frames of backward
+ * calls, one final sum each would be 360+ serial launches per step).  Each of
+ * vsrk_conv_fwd_prelu_bwd / vsrk_prelu_bwd / _pre called with da == NULL
+ * leaves its partials at the start of its workspace; given each call its own
+ * slot of vsrk_slope_slot_doubles() doubles in one zero-filled region per
+ * PReLU, vsrk_slope_final_sum over that region (nparts = slots x slot size)
+ * is the slope gradient of all the calls, summed in slot order (fixed:
+ * deterministic).  pre selects the partials' form (0: output-based, divided
+ * by a^2; 1: pre-activation); one PReLU's calls must all use the same. */
+size_t vsrk_slope_slot_doubles(void);
+int vsrk_slope_final_sum(const double* part, int64_t nparts, const float* a, float* da, int32_t accumulate,
+                         int32_t pre, void* stream);
 
 /* Layout/dtype moves between torch's NC(D)HW fp32 tensors and channels-last
  * views: src is (n, c, d, h, w) fp32 contiguous; channels beyond c in dst are

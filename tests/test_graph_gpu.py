@@ -4,8 +4,10 @@ Adam -- captured into one HIP graph and replayed gives the same parameters as
 the same steps run eagerly.  EDSR (single stream) and DRF (weight gradients on
 a side stream, joined inside the graph).  Captured, DRF cannot read its PReLU
 slopes on the host, so every PReLU backward takes the pre-activation form
-(correct for any slope); the eager reference is put on the same forms, and a
-PReLU with a negative slope is included."""
+(correct for any slope) and one slope-gradient final per call (the eager
+step defers them to one sum per PReLU; under capture that form gave wrong
+slope gradients, tools/diag/graph_drf_grads.py); the eager reference is put
+on the same forms, and a PReLU with a negative slope is included."""
 import pytest
 import torch
 
@@ -21,6 +23,7 @@ def _setup(cls, kw, x_shape, y_shape, seq):
     if cls == "DRFNet":
         net.f_block.up_blocks[0].prelu.weight.data.fill_(-0.1)  # a slope <= 0 (nn.PReLU allows any)
         net._slopes_async = lambda: None  # the captured step's forms, eagerly too
+        net.DEFER_SLOPES = False  # captured, the slope gradients take one final per call: eagerly too
     opt = torch.optim.Adam(net.parameters(), lr=1e-3, capturable=True)
     g = torch.Generator().manual_seed(1)
     if seq:

@@ -138,3 +138,23 @@ def test_drf_fused_prelu_backward_matches_unfused(monkeypatch):
         else:
             err = (gf[k] - v).norm().item() / max(v.norm().item(), 1e-30)
             assert err <= 2e-2, (k, err)
+
+
+def test_deferred_slope_slots_equal_direct():
+    """vsrk_slope_final_sum over per-call slots (da = NULL: the partials stay
+    in each call's slot) gives the slope gradient the direct calls accumulate,
+    within fp32 rounding of the per-call float adds."""
+    g = torch.Generator().manual_seed(21)
+    a = torch.tensor([0.2], device=DEV)
+    S = F.slope_slot_doubles()
+    region = torch.zeros((3, S), dtype=torch.float64, device=DEV)
+    da = torch.zeros(1, device=DEV)
+    for k in range(3):
+        y = torch.randn((2, 1, 9, 21, 64), generator=g).to(DEV, DT)
+        dy = torch.randn(y.shape, generator=g).to(DEV, DT)
+        F.prelu_bwd(y, dy, a, torch.empty_like(y), da, k > 0)
+        F.prelu_bwd(y, dy, a, torch.empty_like(y), None, False, slot=region[k])
+    dd = torch.zeros(1, device=DEV)
+    F.slope_final_sum(region, a, dd, False, False)
+    torch.cuda.synchronize()
+    assert abs(dd.item() - da.item()) <= 1e-5 * (1 + abs(da.item())), (dd.item(), da.item())

@@ -77,6 +77,8 @@ _SIGS = {
     "vsrk_conv_fwd": (C.c_int, [_CD, _T5, _P, _P, _P, _P, _T5, _T5, _T5, _P]),
     "vsrk_conv_fwd_reduce_workspace": (C.c_size_t, [_CD, _T5]),
     "vsrk_conv_prelu_bwd_workspace": (C.c_size_t, []),
+    "vsrk_slope_slot_doubles": (C.c_size_t, []),
+    "vsrk_slope_final_sum": (C.c_int, [_P, C.c_int64, _P, _P, C.c_int32, C.c_int32, _P]),
     "vsrk_conv_fwd_prelu_bwd": (C.c_int, [_CD, _T5, _P, _P, _T5, _T5, C.c_int32, _P, C.c_int32, _P, C.c_size_t,
                                           _P]),
     "vsrk_conv_fwd_reduce": (C.c_int, [_CD, _T5, _P, _P, _P, _P, _T5, C.c_int32, _T5, _P, _P, _P, _P, _P, _P, _P,

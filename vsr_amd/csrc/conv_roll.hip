@@ -76,6 +76,11 @@ __device__ __forceinline__ uint4 roll_bload16(RRsrc r, uint32_t off) {
 #ifndef ROLL_PREF2D
 #define ROLL_PREF2D 1
 #endif
+// SWAP_PREF: the register-transposed flush also for the prefetched residual /
+// mask forms (their prefetch then in the swap lanes' layout)
+#ifndef ROLL_SWAP_PREF
+#define ROLL_SWAP_PREF 0
+#endif
 
 namespace {
 using namespace vsrk_conv;
@@ -266,7 +271,7 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
   // (3-D: the BN input of RE_BNRED, read by the flush of the slice's finished depth)
   constexpr bool PREF = (ROLL_PREF2D && KD == 1 && ((EM & RE_RES) != 0) != ((EM & RE_MASK) != 0) && !(EM & RE_ACC)) ||
                         (KD == 3 && (EM & RE_BNRED) != 0);
-  constexpr bool SWAP = ROLL_SWAP && KD == 1 && !PREF;
+  constexpr bool SWAP = ROLL_SWAP && KD == 1 && (!PREF || ROLL_SWAP_PREF);
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hf = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -531,10 +536,11 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
         const int ho = tl.h0 + wave * RMS + ms;
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-          const int wo = tl.w0 + tv + 16 * k;
+          // (SWAP: the lanes of epilogue_sw -- voxel (r & 15) + 16 k, chunk ecc)
+          const int wo = tl.w0 + (SWAP ? (r & 15) : tv) + 16 * k;
           const bool ok = ho < a.y.h && wo < a.y.w;
           const H* pp = reinterpret_cast<const H*>(pv.ptr) +
-                        (tl.nb * pv.sn + dz * pv.sd + ho * pv.sh + wo * pv.sw + tl.n0 + 8 * tc8);
+                        (tl.nb * pv.sn + dz * pv.sd + ho * pv.sh + wo * pv.sw + tl.n0 + 8 * (SWAP ? 2 * (r >> 4) + hf : tc8));
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt) {
             const void* src = ok ? (const void*)(pp + nt * 32) : (const void*)zp;
@@ -840,7 +846,7 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
   // out-of-range voxels take a buffer offset past the resource (loads read
   // zero, stores are dropped).
   const int ecc = 2 * (r >> 4) + hf;
-  auto epilogue_sw = [&](const f32x16 (&A)[RMS], const RTile& tl, int dz, int nt) __attribute__((always_inline)) {
+  auto epilogue_sw = [&](const f32x16 (&A)[RMS], const RTile& tl, int dz, int nt, bool use_pre) __attribute__((always_inline)) {
     const int64_t sbase = (int64_t)tl.nb * a.y.sn + (int64_t)dz * a.y.sd;
     const RRsrc ry = roll_rsrc(reinterpret_cast<const H*>(a.y.ptr) + sbase);
     // (RE_PMASK: the mask has y's geometry and strides, the host checks)
@@ -893,7 +899,10 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
         }
         if constexpr (EM & RE_MASK) {
           float m[8];
-          Chunk<H>::unpack(roll_bload16(rmk, ok ? 2u * (uint32_t)(ho * a.msk.sh + wo * a.msk.sw + co) : ROLL_OOB), m);
+          uint4 mv;
+          if (PREF && use_pre) mv = __builtin_bit_cast(uint4, pre[PREF ? ms : 0][PREF ? nt : 0][q]);
+          else mv = roll_bload16(rmk, ok ? 2u * (uint32_t)(ho * a.msk.sh + wo * a.msk.sw + co) : ROLL_OOB);
+          Chunk<H>::unpack(mv, m);
 #pragma unroll
           for (int e = 0; e < 8; ++e) t[e] = m[e] > 0.f ? t[e] : 0.f;
         }
@@ -916,7 +925,10 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
         }
         if constexpr (EM & RE_RES) {
           float rr[8];
-          Chunk<H>::unpack(roll_bload16(rrs, ok ? 2u * (uint32_t)(ho * a.res.sh + wo * a.res.sw + co) : ROLL_OOB), rr);
+          uint4 rv;
+          if (PREF && use_pre) rv = __builtin_bit_cast(uint4, pre[PREF ? ms : 0][PREF ? nt : 0][q]);
+          else rv = roll_bload16(rrs, ok ? 2u * (uint32_t)(ho * a.res.sh + wo * a.res.sw + co) : ROLL_OOB);
+          Chunk<H>::unpack(rv, rr);
 #pragma unroll
           for (int e = 0; e < 8; ++e) t[e] += rr[e];
         }
@@ -979,7 +991,7 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
 #pragma unroll
       for (int b = 0; b < NACC; ++b) {
         if (!(ROLL_ABL & 4) && P >= tl.z0 && P < tl.z1) {
-          if constexpr (SWAP) epilogue_sw(acc[b], tl, P, b);
+          if constexpr (SWAP) epilogue_sw(acc[b], tl, P, b, use_pre);
           else epilogue_tr(acc[b], tl, P, b, use_pre ? EO_PRE : EO_LOAD, scr);
         }
 #pragma unroll
@@ -1654,7 +1666,7 @@ extern "C" int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* d, const vsrk_tenso
                                        const float* bias, const vsrk_tensor5* y_fwd, const vsrk_tensor5* y,
                                        int32_t c_lo, float* da, int32_t accumulate_da, void* workspace,
                                        size_t workspace_bytes, void* stream) {
-  VSRK_CHECK(d && x && y && y_fwd && w_packed && d->mask_slope && da, "conv_fwd_prelu_bwd: null argument");
+  VSRK_CHECK(d && x && y && y_fwd && w_packed && d->mask_slope, "conv_fwd_prelu_bwd: null argument");
   VSRK_CHECK(workspace && workspace_bytes >= vsrk_conv_prelu_bwd_workspace(),
              "conv_fwd_prelu_bwd: workspace %zu < %zu bytes", workspace_bytes, vsrk_conv_prelu_bwd_workspace());
   VSRK_CHECK(((uintptr_t)workspace & 15) == 0, "conv_fwd_prelu_bwd: workspace must be 16-byte aligned");
@@ -1677,8 +1689,10 @@ extern "C" int vsrk_conv_fwd_prelu_bwd(const vsrk_conv_desc* d, const vsrk_tenso
   }
   if (rc == 0) return VSRK_ERR_UNSUPPORTED;
   if (rc < 0) return -rc;
-  vsrk_slope_final((const double*)workspace, nparts, d->mask_slope, da, accumulate_da, 0, s);
-  VSRK_LAUNCH_CHECK("conv_fwd_prelu_bwd_final");
+  if (da) {  // (da == NULL: the partials stay in the workspace slot, vsrk_slope_final_sum later)
+    vsrk_slope_final((const double*)workspace, nparts, d->mask_slope, da, accumulate_da, 0, s);
+    VSRK_LAUNCH_CHECK("conv_fwd_prelu_bwd_final");
+  }
   return VSRK_OK;
 }
 

@@ -200,6 +200,18 @@ void vsrk_slope_final(const double* part, int nparts, const float* a, float* da,
   slope_final_kernel<<<1, 256, 0, s>>>(part, nparts, a, da, accumulate, pre);
 }
 
+extern "C" size_t vsrk_slope_slot_doubles(void) {  // the most partials any PReLU backward entry point writes
+  return std::max<size_t>(PRELU_BLOCKS, std::max(vsrk_roll_slope_ws_bytes(), vsrk_pw_pbwd_ws_bytes()) / sizeof(double));
+}
+
+extern "C" int vsrk_slope_final_sum(const double* part, int64_t nparts, const float* a, float* da,
+                                    int32_t accumulate, int32_t pre, void* stream) {
+  VSRK_CHECK(part && a && da && nparts >= 0 && nparts < (1ll << 31), "slope_final_sum: bad argument");
+  vsrk_slope_final(part, (int)nparts, a, da, accumulate, pre, (hipStream_t)stream);
+  VSRK_LAUNCH_CHECK("slope_final_sum");
+  return VSRK_OK;
+}
+
 extern "C" size_t vsrk_prelu_workspace_size(void) { return PRELU_BLOCKS * sizeof(double); }
 
 extern "C" int vsrk_prelu_wgrad(const vsrk_tensor5* y, const vsrk_tensor5* dx, const float* a, float* da,
@@ -365,7 +377,7 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(View y, View dy, View dy
 static int prelu_bwd_impl(const vsrk_tensor5* y, const vsrk_tensor5* dy, const vsrk_tensor5* dy2, const float* a,
                           const vsrk_tensor5* dx, float* da, int32_t accumulate_da, void* workspace,
                           size_t workspace_bytes, void* stream, int pre) {
-  VSRK_CHECK(y && dy && dx && a && da && y->ptr && dy->ptr && dx->ptr, "prelu_bwd: null argument");
+  VSRK_CHECK(y && dy && dx && a && y->ptr && dy->ptr && dx->ptr, "prelu_bwd: null argument");
   for (const vsrk_tensor5* t : {dy, dy2, dx}) {
     if (!t) continue;
     VSRK_CHECK(t->dtype == y->dtype && t->n == y->n && t->d == y->d && t->h == y->h && t->w == y->w &&
@@ -395,8 +407,10 @@ static int prelu_bwd_impl(const vsrk_tensor5* y, const vsrk_tensor5* dy, const v
   else
     prelu_bwd_kernel<float><<<PRELU_BLOCKS, 256, 0, s>>>(vy, vg, vg2, dy2 != nullptr, a, vo, (int)nr64, vec, part, pre);
   VSRK_LAUNCH_CHECK("prelu_bwd");
-  vsrk_slope_final(part, PRELU_BLOCKS, a, da, accumulate_da, pre, s);
-  VSRK_LAUNCH_CHECK("prelu_final");
+  if (da) {  // (da == NULL: the partials stay in the workspace slot, vsrk_slope_final_sum later)
+    vsrk_slope_final(part, PRELU_BLOCKS, a, da, accumulate_da, pre, s);
+    VSRK_LAUNCH_CHECK("prelu_final");
+  }
   return VSRK_OK;
 }
 

@@ -21,7 +21,8 @@ __all__ = [
     "loss_fwd", "loss_bwd", "psnr", "ssim", "workspace", "LOSS_KINDS",
     "bn_stats", "bn_finalize", "bn_fold_running", "bn_apply", "bn_relu_bwd_reduce", "bn_relu_bwd_apply",
     "duf_dynfilter_fwd", "duf_dynfilter_bwd",
-    "subpixel_conv_weight", "subpixel_wgrad_fold", "prelu_wgrad", "prelu_bwd",
+    "subpixel_conv_weight", "subpixel_wgrad_fold", "prelu_wgrad", "prelu_bwd", "slope_slot_doubles",
+    "slope_final_sum",
 ]
 
 LOSS_KINDS = {"L1Loss": 0, "MSELoss": 1, "HuberLoss": 2, "CharbonnierLoss": 3}
@@ -130,6 +131,9 @@ def view_bytes(v) -> float:
     return float(v.n) * v.d * v.h * v.w * v.c * (4 if v.dtype == N.VSRK_F32 else 2)
 
 
+_ws_kept: list = []
+
+
 def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
     """A scratch buffer per (device, current stream): grown on demand, reused in
     stream order (the nets run weight gradients on a second stream, which
@@ -138,6 +142,11 @@ def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
     key = (dev, torch.cuda.current_stream(dev).cuda_stream)
     buf = _ws.get(key)
     if buf is None or buf.numel() < nbytes:
+        if buf is not None and torch.cuda.is_current_stream_capturing():
+            # inside a graph capture a freed block can go to the next captured
+            # allocation on another stream while this stream's kernels still
+            # use it: the outgrown buffer is kept
+            _ws_kept.append(buf)
         buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
         _ws[key] = buf
     return buf
@@ -273,22 +282,24 @@ def _launched(rc) -> bool:
 
 def conv_prelu_bwd(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, k, pad, y_fwd: torch.Tensor,
                    a: torch.Tensor, da: torch.Tensor, accumulate_da: bool, *, x_shuffle: int = 1, y_shuffle: int = 1,
-                   subpixel: int = 0, accumulate: bool = False, c_lo: int = 0) -> bool:
+                   subpixel: int = 0, accumulate: bool = False, c_lo: int = 0,
+                   slot: torch.Tensor | None = None) -> bool:
     """y = (conv(x) [+ y]) * (y_fwd > 0 ? 1 : a) on channels >= c_lo and da
     [+]= the PReLU slope gradient (vsrk_conv_fwd_prelu_bwd): conv [accumulate]
     followed by prelu_bwd(y_fwd, y, a, y, da) on y[..., c_lo:] in one kernel.
-    False when the shape is not eligible (nothing launched)."""
+    False when the shape is not eligible (nothing launched).  slot: keep the
+    slope partials there instead (see prelu_bwd; da unused)."""
     if not FUSE:
         return False
     lib = _lib()
     d = _desc(k, pad, accumulate=accumulate, mask_slope=a, subpixel=subpixel)
     xv, yv, mv = N.t5(x, x_shuffle), N.t5(y, y_shuffle), N.t5(y_fwd, y_shuffle)
-    ws = workspace(lib.vsrk_conv_prelu_bwd_workspace(), y.device)
+    ws = slot if slot is not None else workspace(lib.vsrk_conv_prelu_bwd_workspace(), y.device)
     nbytes = ws.numel() * ws.element_size()
 
     def launch():
         return lib.vsrk_conv_fwd_prelu_bwd(C.byref(d), C.byref(xv), wp.data_ptr(), None, C.byref(mv), C.byref(yv),
-                                           int(c_lo), da.data_ptr(),
+                                           int(c_lo), None if slot is not None else da.data_ptr(),
                                            1 if accumulate_da else 0, ws.data_ptr(), nbytes, N.stream_ptr(y.device))
 
     rc = (timer.wrap(("conv_fwd", tuple(k)), xv, yv, launch, _launched,
@@ -738,23 +749,37 @@ def prelu_wgrad(y: torch.Tensor, dx: torch.Tensor, a: torch.Tensor, da: torch.Te
 
 
 def prelu_bwd(y: torch.Tensor, dy: torch.Tensor, a: torch.Tensor, dx: torch.Tensor, da: torch.Tensor | None,
-              accumulate_da: bool, dy2: torch.Tensor | None = None, pre: bool = False) -> torch.Tensor:
+              accumulate_da: bool, dy2: torch.Tensor | None = None, pre: bool = False,
+              slot: torch.Tensor | None = None) -> torch.Tensor:
     """dx = (dy [+ dy2]) * (y > 0 ? 1 : a); da [+]= sum_{y<0} dx*y/a^2 (one
     pass) for the PReLU output y (exact while a > 0).  pre=True: y is the
     pre-activation x (vsrk_prelu_bwd_pre, any slope): dx = g (x > 0 ? 1 : a),
-    da [+]= sum_{x<0} g x with g = dy [+ dy2]."""
+    da [+]= sum_{x<0} g x with g = dy [+ dy2].  slot: a zero-filled float64
+    tensor of slope_slot_doubles() elements that keeps this call's slope
+    partials instead (da unused; slope_final_sum later)."""
     lib = _lib()
-    ws = workspace(lib.vsrk_prelu_workspace_size(), y.device)
+    ws = slot if slot is not None else workspace(lib.vsrk_prelu_workspace_size(), y.device)
     nbytes = ws.numel() * ws.element_size()
     yv, gv, ov = N.t5(y), N.t5(dy), N.t5(dx)
     g2 = N.t5(dy2) if dy2 is not None else None
     fn = lib.vsrk_prelu_bwd_pre if pre else lib.vsrk_prelu_bwd
     N.check(fn(C.byref(yv), C.byref(gv), C.byref(g2) if g2 is not None else None, a.data_ptr(),
-               C.byref(ov), da.data_ptr(), 1 if accumulate_da else 0, ws.data_ptr(),
+               C.byref(ov), None if slot is not None else da.data_ptr(), 1 if accumulate_da else 0, ws.data_ptr(),
                nbytes, N.stream_ptr(y.device)), "prelu_bwd_pre" if pre else "prelu_bwd")
     return dx
 
 
+def slope_slot_doubles() -> int:
+    """float64 elements of one deferred PReLU slope-partial slot."""
+    return int(_lib().vsrk_slope_slot_doubles())
+
+
+def slope_final_sum(part: torch.Tensor, a: torch.Tensor, da: torch.Tensor, accumulate: bool, pre: bool) -> None:
+    """da [+]= the slope gradient of every deferred call whose slot lies in
+    part (float64, zero-filled before the calls), summed in slot order."""
+    N.check(_lib().vsrk_slope_final_sum(part.data_ptr(), part.numel(), a.data_ptr(), da.data_ptr(),
+                                        1 if accumulate else 0, 1 if pre else 0, N.stream_ptr(part.device)),
+            "slope_final_sum")
 
 
 # ------------------------------------------------------------ device peaks --

@@ -156,8 +156,15 @@ class _DRFBase(BaseNet):
     # the PReLU backwards over concat-gradient slices fused into their last
     # producer (round 5; VSR_DRF_FUSE_SLICES=0 for A/B)
     FUSE_SLICES = os.environ.get("VSR_DRF_FUSE_SLICES", "1") != "0"
+    # training: the in_block convs once over all frames (VSR_DRF_BATCH_IN=0 for A/B)
+    BATCH_IN_BLOCK = os.environ.get("VSR_DRF_BATCH_IN", "1") != "0"
+    # eager training: every PReLU backward call leaves its slope partials in a
+    # per-(PReLU, frame) slot, one fixed-order sum per PReLU after the
+    # recurrence (VSR_DRF_DEFER_SLOPES=0: one final per call)
+    DEFER_SLOPES = os.environ.get("VSR_DRF_DEFER_SLOPES", "1") != "0"
     def __init__(self, in_channels, out_channels, num_features, num_groups, upscale_factor):
         super().__init__()
+        self._sp_tmp: dict = {}  # side-stream scratch of the sub-pixel weight gradients
         self.in_channels = in_channels
         self.out_channels = out_channels
         self.num_features = num_features
@@ -261,11 +268,24 @@ class _DRFBase(BaseNet):
             XV = F.to_view(torch.cat([x.float() for x in frames]), cd, cpad=8)[..., :cin]  # (T*b, 1, h, w, cin)
         outs, recs = [], []
         X0 = buf("X0", 0, h, w, 2 * f, T + 1)
+        batched = seqs is not None and self.BATCH_IN_BLOCK
+        if batched:
+            # in_features = in_block(x_t) does not depend on the recurrence
+            # (drf_net.py:40-41): both in_block convs run once over all T
+            # frames of the sequence buffers (per frame they were 2 x T small
+            # latency-bound launches)
+            buf("u1", 0, h, w, 4 * f)  # creates the (T, B, h, w, 4F) sequence buffer
+            U1 = seqs["u1"].view(T * b, 1, h, w, 4 * f)
+            F.conv(XV, pw(ib.conv1), U1, K3, P1, bias=ib.conv1.bias, act=PR, act_param=ib.prelu1.weight)
+            X0s = seqs["X0"][:T].view(T * b, 1, h, w, 2 * f)
+            F.conv(U1, pw(ib.conv2), X0s[..., :f], K1, P0, bias=ib.conv2.bias, act=PR, act_param=ib.prelu2.weight)
         for t, x in enumerate(frames):
             xv = XV[t * b:(t + 1) * b] if XV is not None else F.to_view(x, cd, cpad=8)[..., :cin]
             u1 = buf("u1", t, h, w, 4 * f)
-            F.conv(xv, pw(ib.conv1), u1, K3, P1, bias=ib.conv1.bias, act=PR, act_param=ib.prelu1.weight)
-            F.conv(u1, pw(ib.conv2), X0[..., :f], K1, P0, bias=ib.conv2.bias, act=PR, act_param=ib.prelu2.weight)
+            if not batched:
+                F.conv(xv, pw(ib.conv1), u1, K3, P1, bias=ib.conv1.bias, act=PR, act_param=ib.prelu1.weight)
+                F.conv(u1, pw(ib.conv2), X0[..., :f], K1, P0, bias=ib.conv2.bias, act=PR,
+                       act_param=ib.prelu2.weight)
             if t == 0:  # hidden_state = in_features (drf_net.py:42-43)
                 F.conv(u1, pw(ib.conv2), X0[..., f:], K1, P0, bias=ib.conv2.bias, act=PR,
                        act_param=ib.prelu2.weight)
@@ -478,8 +498,14 @@ class _DRFBase(BaseNet):
             db, _ = gbuf(conv.bias)
 
             def run(x_, dy_, acc_):  # the sub-pixel wgrad and its fold
-                dweq = torch.empty((cop, cip, 1, 3, 3), dtype=torch.float32, device=dev)
-                dbeq = torch.empty(cop, dtype=torch.float32, device=dev)
+                # (persistent side-stream scratch: inside a graph capture a
+                # block freed on one stream can go to the next captured
+                # allocation on the other one while kernels still use it)
+                tk = (cop, cip, dev)
+                if tk not in self._sp_tmp:
+                    self._sp_tmp[tk] = (torch.empty((cop, cip, 1, 3, 3), dtype=torch.float32, device=dev),
+                                        torch.empty(cop, dtype=torch.float32, device=dev))
+                dweq, dbeq = self._sp_tmp[tk]
                 spc = F.subpixel_code(k_, s_, p_, transposed, False)
                 if transposed:
                     F.conv_wgrad(x_, dy_, K3, P1, dweq, dbeq, dy_shuffle=s_, subpixel=spc)
@@ -489,28 +515,57 @@ class _DRFBase(BaseNet):
 
             defer(conv.weight, t, x, dy, run, acc)
 
+        # PReLU slope gradients, deferred: every PReLU backward call of frame
+        # t leaves its partials in slot t of its PReLU's zero-filled region;
+        # one fixed-order sum per PReLU after the loop (12 launches per step
+        # instead of one final per call, 540 at cfg 3)
+        S = F.slope_slot_doubles()
+        regions: dict = {}  # id(prelu) -> (prelu, (T, S) float64, frames taken)
+        cur = [T - 1]
+
+        # Inside a graph capture the slope gradients are not deferred: with
+        # the slot regions the captured step's slope gradients came out wrong
+        # (every other gradient bitwise equal to the eager step's;
+        # tools/diag/graph_drf_grads.py), cause open -- the per-call finals
+        # below are what the captured-vs-eager test holds equal
+        defer_slopes = self.DEFER_SLOPES and not torch.cuda.is_current_stream_capturing()
+
+        def slot_row(pr):
+            reg = regions.get(id(pr))
+            if reg is None:
+                reg = regions[id(pr)] = (pr, torch.zeros((T, S), dtype=torch.float64, device=dev), set())
+            if cur[0] in reg[2]:
+                raise RuntimeError("DRF backward: two slope-gradient calls of one PReLU in one frame")
+            reg[2].add(cur[0])
+            return reg[1][cur[0]]
+
+        def slot(pr):
+            """(da, accumulate_da, slot) of a PReLU backward call: deferred,
+            the call's slot row; else its slope gradient buffer"""
+            if defer_slopes:
+                return None, False, slot_row(pr)
+            da, acc = gbuf(pr.weight)
+            return da, acc, None
+
         def fuse(pr, call) -> bool:
             """the PReLU pr's backward fused into its gradient's last producer:
-            call(da, accumulate_da) -> launched (F.conv_prelu_bwd); never for a
-            slope <= 0 (the fused epilogues read the PReLU output)"""
-            if id(pr) in nonpos or not self.FUSE_SLICES:
+            call(slot) -> launched (F.conv_prelu_bwd); never for a slope <= 0
+            (the fused epilogues read the PReLU output)"""
+            if id(pr) in nonpos or not self.FUSE_SLICES or not defer_slopes:
                 return False
-            existed = id(pr.weight) in bufs
-            da, acc = gbuf(pr.weight)
-            if call(da, acc):
+            if call(slot_row(pr)):
                 return True
-            if not existed:  # nothing written: the unfused backward starts da
-                del bufs[id(pr.weight)]
+            regions[id(pr)][2].discard(cur[0])  # nothing launched: the slot stays free (and zero)
             return False
 
         def prelu(y, dy, pr, out, dy2=None, pre=None):
             """PReLU backward from its output y; for a slope <= 0 from the
             pre-activation that pre() recomputes from the tape (the producing
             conv without its activation), as nn.PReLU does (drf_net.py:55-58)"""
-            da, acc = gbuf(pr.weight)
+            da_, acc_, sl_ = slot(pr)
             if id(pr) in nonpos:
-                return F.prelu_bwd(pre(), dy, pr.weight, out, da, acc, dy2=dy2, pre=True)
-            return F.prelu_bwd(y, dy, pr.weight, out, da, acc, dy2=dy2)
+                return F.prelu_bwd(pre(), dy, pr.weight, out, da_, acc_, dy2=dy2, pre=True, slot=sl_)
+            return F.prelu_bwd(y, dy, pr.weight, out, da_, acc_, dy2=dy2, slot=sl_)
 
         co = self.out_channels
         HH, WW = recs[0]["tail_in"].shape[2], recs[0]["tail_in"].shape[3]
@@ -519,6 +574,7 @@ class _DRFBase(BaseNet):
         GV = F.to_view(torch.cat([g_.float() for g_ in gfull]), cd, cpad=8)[..., :co]  # (T*b, 1, HH, WW, co)
         d_hidden = None  # grad of the previous frame's f_features (X0_t[..., f:])
         for t in range(T - 1, -1, -1):
+            cur[0] = t
             rc = recs[t]
             u = rc["tail_in"]
             hh, ww = u.shape[2], u.shape[3]
@@ -561,8 +617,8 @@ class _DRFBase(BaseNet):
                 return fb.up_blocks[i_].prelu if i_ == 0 else fb.up_blocks[i_].prelu2
 
             wo = pw(fb.out_block.conv, 1)
-            if fuse(dnpr(G - 1), lambda da, acc: F.conv_prelu_bwd(
-                    gout, wo, dL[..., f:], K1, P0, L[..., f:], dnpr(G - 1).weight, da, acc, c_lo=(G - 1) * f)):
+            if fuse(dnpr(G - 1), lambda sl_: F.conv_prelu_bwd(
+                    gout, wo, dL[..., f:], K1, P0, L[..., f:], dnpr(G - 1).weight, None, False, c_lo=(G - 1) * f, slot=sl_)):
                 done.add(("l", G - 1))
             else:
                 F.conv(gout, wo, dL[..., f:], K1, P0)
@@ -582,28 +638,28 @@ class _DRFBase(BaseNet):
                 wq1, _ = sp(cv, False, 1)
                 spc = F.subpixel_code(k, s, p, False, True)
                 if i == 0:
-                    if fuse(uppr(0), lambda da, acc: F.conv_prelu_bwd(
-                            gl, wq1, dHc[..., :f], K3, P1, Hc[..., :f], uppr(0).weight, da, acc, y_shuffle=s,
-                            subpixel=spc, accumulate=G > 1)):
+                    if fuse(uppr(0), lambda sl_: F.conv_prelu_bwd(
+                            gl, wq1, dHc[..., :f], K3, P1, Hc[..., :f], uppr(0).weight, None, False, y_shuffle=s,
+                            subpixel=spc, accumulate=G > 1, slot=sl_)):
                         done.add(("h", 0))
                     else:
                         F.conv(gl, wq1, dHc[..., :f], K3, P1, y_shuffle=s, accumulate=G > 1, subpixel=spc)
                 else:
                     dt2 = sbuf(f"dt2_{i}", t, H, W, f)
-                    da, acc = gbuf(dn.prelu1.weight)
+                    da2, acc2, sl2 = slot(dn.prelu1)
                     if id(dn.prelu1) in nonpos:  # slope <= 0: from the recomputed pre-activation
                         F.conv(gl, wq1, dt2, K3, P1, y_shuffle=s, subpixel=spc)
                         x2 = F.conv(Hc[..., :(i + 1) * f], pw(dn.conv1), new(H, W, f), K1, P0, bias=dn.conv1.bias)
-                        F.prelu_bwd(x2, dt2, dn.prelu1.weight, dt2, da, acc, pre=True)
-                    elif not F.conv_prelu_bwd(gl, wq1, dt2, K3, P1, rc["t2s"][i], dn.prelu1.weight, da, acc,
-                                              y_shuffle=s, subpixel=spc):
+                        F.prelu_bwd(x2, dt2, dn.prelu1.weight, dt2, da2, acc2, pre=True, slot=sl2)
+                    elif not F.conv_prelu_bwd(gl, wq1, dt2, K3, P1, rc["t2s"][i], dn.prelu1.weight, da2, acc2,
+                                              y_shuffle=s, subpixel=spc, slot=sl2):
                         F.conv(gl, wq1, dt2, K3, P1, y_shuffle=s, subpixel=spc)
-                        F.prelu_bwd(rc["t2s"][i], dt2, dn.prelu1.weight, dt2, da, acc)
+                        F.prelu_bwd(rc["t2s"][i], dt2, dn.prelu1.weight, dt2, da2, acc2, slot=sl2)
                     wgrad(dn.conv1, Hc[..., :(i + 1) * f], dt2, K1, P0, t)
                     wd1 = pw(dn.conv1, 1)
-                    if fuse(uppr(i), lambda da, acc: F.conv_prelu_bwd(
-                            dt2, wd1, dHc[..., :(i + 1) * f], K1, P0, Hc[..., :(i + 1) * f], uppr(i).weight, da, acc,
-                            accumulate=i != G - 1, c_lo=i * f)):
+                    if fuse(uppr(i), lambda sl_: F.conv_prelu_bwd(
+                            dt2, wd1, dHc[..., :(i + 1) * f], K1, P0, Hc[..., :(i + 1) * f], uppr(i).weight, None, False,
+                            accumulate=i != G - 1, c_lo=i * f, slot=sl_)):
                         done.add(("h", i))
                     else:
                         F.conv(dt2, wd1, dHc[..., :(i + 1) * f], K1, P0, accumulate=i != G - 1)
@@ -622,29 +678,29 @@ class _DRFBase(BaseNet):
                 spc = F.subpixel_code(k, s, p, True, True)
                 if i == 0:
                     ipr = fb.in_block.prelu
-                    if fuse(ipr, lambda da, acc: F.conv_prelu_bwd(
-                            gh, wq1, dL[..., :f], K3, P1, L[..., :f], ipr.weight, da, acc, x_shuffle=s,
-                            subpixel=spc, accumulate=True)):
+                    if fuse(ipr, lambda sl_: F.conv_prelu_bwd(
+                            gh, wq1, dL[..., :f], K3, P1, L[..., :f], ipr.weight, None, False, x_shuffle=s,
+                            subpixel=spc, accumulate=True, slot=sl_)):
                         done.add("g0")
                     else:
                         F.conv(gh, wq1, dL[..., :f], K3, P1, x_shuffle=s, accumulate=True, subpixel=spc)
                 else:
                     dt1 = sbuf(f"dt1_{i}", t, h, w, f)
-                    da, acc = gbuf(up.prelu1.weight)
+                    da1, acc1, sl1 = slot(up.prelu1)
                     if id(up.prelu1) in nonpos:  # slope <= 0: from the recomputed pre-activation
                         F.conv(gh, wq1, dt1, K3, P1, x_shuffle=s, subpixel=spc)
                         x1 = F.conv(L[..., :(i + 1) * f], pw(up.conv1), new(h, w, f), K1, P0, bias=up.conv1.bias)
-                        F.prelu_bwd(x1, dt1, up.prelu1.weight, dt1, da, acc, pre=True)
-                    elif not F.conv_prelu_bwd(gh, wq1, dt1, K3, P1, rc["t1s"][i], up.prelu1.weight, da, acc,
-                                              x_shuffle=s, subpixel=spc):
+                        F.prelu_bwd(x1, dt1, up.prelu1.weight, dt1, da1, acc1, pre=True, slot=sl1)
+                    elif not F.conv_prelu_bwd(gh, wq1, dt1, K3, P1, rc["t1s"][i], up.prelu1.weight, da1, acc1,
+                                              x_shuffle=s, subpixel=spc, slot=sl1):
                         F.conv(gh, wq1, dt1, K3, P1, x_shuffle=s, subpixel=spc)
-                        F.prelu_bwd(rc["t1s"][i], dt1, up.prelu1.weight, dt1, da, acc)
+                        F.prelu_bwd(rc["t1s"][i], dt1, up.prelu1.weight, dt1, da1, acc1, slot=sl1)
                     wgrad(up.conv1, L[..., :(i + 1) * f], dt1, K1, P0, t)
                     wu1 = pw(up.conv1, 1)
                     # the last contribution to lr_i's gradient (slice i of dL)
-                    if fuse(dnpr(i - 1), lambda da, acc: F.conv_prelu_bwd(
-                            dt1, wu1, dL[..., :(i + 1) * f], K1, P0, L[..., :(i + 1) * f], dnpr(i - 1).weight, da,
-                            acc, accumulate=True, c_lo=i * f)):
+                    if fuse(dnpr(i - 1), lambda sl_: F.conv_prelu_bwd(
+                            dt1, wu1, dL[..., :(i + 1) * f], K1, P0, L[..., :(i + 1) * f], dnpr(i - 1).weight, None,
+                            False, accumulate=True, c_lo=i * f, slot=sl_)):
                         done.add(("l", i - 1))
                     else:
                         F.conv(dt1, wu1, dL[..., :(i + 1) * f], K1, P0, accumulate=True)
@@ -664,13 +720,16 @@ class _DRFBase(BaseNet):
             wgrad(ib.conv2, rc["u1"], gin, K1, P0, t)
             du1 = sbuf("du_u1", t, h, w, 4 * f)
             wi2 = pw(ib.conv2, 1)
-            if not fuse(ib.prelu1, lambda da, acc: F.conv_prelu_bwd(gin, wi2, du1, K1, P0, rc["u1"], ib.prelu1.weight,
-                                                                      da, acc)):
+            if not fuse(ib.prelu1, lambda sl_: F.conv_prelu_bwd(gin, wi2, du1, K1, P0, rc["u1"], ib.prelu1.weight,
+                                                                    None, False, slot=sl_)):
                 F.conv(gin, wi2, du1, K1, P0)
                 prelu(rc["u1"], du1, ib.prelu1, du1,
                       pre=lambda: F.conv(rc["xv"], pw(ib.conv1), new(h, w, 4 * f), K3, P1, bias=ib.conv1.bias))
             wgrad(ib.conv1, rc["xv"], du1, K3, P1, t)
             launch_runs(t)
+        for pr, reg, _ in regions.values():  # the slope gradients, one fixed-order sum per PReLU
+            da, acc = gbuf(pr.weight)
+            F.slope_final_sum(reg, pr.weight, da, acc, id(pr) in nonpos)
         for prm, g in bufs.values():
             self._grad_done(grads, prm, g)
         return grads
