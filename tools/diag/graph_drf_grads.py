@@ -1,6 +1,6 @@
 """Captured vs eager DRF train step (tests/test_graph_gpu.py's f = 32 case):
-per-parameter gradient differences after ONE replay and one eager step, to
-find where the two first part."""
+per-parameter gradient differences after each of three replays / eager
+steps, to find where the two first part."""
 import sys
 from pathlib import Path
 
@@ -25,10 +25,15 @@ for (k, p), (_, q) in zip(net.named_parameters(), ref_net.named_parameters()):
 graph = torch.cuda.CUDAGraph()
 with torch.cuda.graph(graph):
     step()
-graph.replay()
-ref_step()
-torch.cuda.synchronize()
-for (k, p), (_, q) in zip(net.named_parameters(), ref_net.named_parameters()):
-    g, h = p.grad, q.grad
-    d = (g - h).abs().max().item()
-    print(f"{k:45s} grad max|d| {d:.3e}  |g| {h.abs().max().item():.3e}  param equal {torch.equal(p, q)}")
+for it in range(3):
+    graph.replay()
+    ref_step()
+    torch.cuda.synchronize()
+    bad = []
+    for (k, p), (_, q) in zip(net.named_parameters(), ref_net.named_parameters()):
+        d = (p.grad - q.grad).abs().max().item()
+        if d > 0 or not torch.equal(p, q):
+            bad.append(f"{k} grad max|d| {d:.3e} |g| {q.grad.abs().max().item():.3e} param equal {torch.equal(p, q)}")
+    print(f"replay {it}: {len(bad)} parameters differ")
+    for b in bad[:40]:
+        print("  ", b)

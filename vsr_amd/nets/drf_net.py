@@ -524,10 +524,12 @@ class _DRFBase(BaseNet):
         cur = [T - 1]
 
         # Inside a graph capture the slope gradients are not deferred: with
-        # the slot regions the captured step's slope gradients came out wrong
-        # (every other gradient bitwise equal to the eager step's;
-        # tools/diag/graph_drf_grads.py), cause open -- the per-call finals
-        # below are what the captured-vs-eager test holds equal
+        # the slot regions the captured step's slope gradients come out wrong
+        # while every other gradient stays bitwise equal to the eager step's
+        # (tools/diag/graph_drf_grads.py; persistent slot regions, persistent
+        # side-stream scratch and kept workspaces did not change it: cause
+        # open) -- the per-call finals are what the captured-vs-eager test
+        # holds equal
         defer_slopes = self.DEFER_SLOPES and not torch.cuda.is_current_stream_capturing()
 
         def slot_row(pr):
