@@ -78,6 +78,11 @@ __device__ __forceinline__ uint4 roll_bload16(RRsrc r, uint32_t off) {
 #endif
 // SWAP_PREF: the register-transposed flush also for the prefetched residual /
 // mask forms (their prefetch then in the swap lanes' layout)
+// PFEARLY: the 2-D operand prefetch issued this many stages earlier than the
+// slice's third-to-last (A/B knob)
+#ifndef ROLL_PFEARLY
+#define ROLL_PFEARLY 0
+#endif
 #ifndef ROLL_SWAP_PREF
 #define ROLL_SWAP_PREF 0
 #endif
@@ -1129,7 +1134,7 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
           prefetch(ct, pz);
           pf_slice = true;
         }
-      } else if (cc == max(a.nchunk - 3, 0) && out_in) {
+      } else if (cc == max(a.nchunk - 3 - ROLL_PFEARLY, 0) && out_in) {
         pf_next = true;
       }
     }
@@ -1150,7 +1155,7 @@ __global__ __launch_bounds__(RNW * 64, RNW / 4) void conv_roll_kernel(RollArgs a
       if (pf_next) {
         prefetch(ct, pz);
         pf_slice = true;
-        pf_hold = min(2, a.nchunk - 1);
+        pf_hold = min(2 + ROLL_PFEARLY, a.nchunk - 1);
       }
     }
     // the stage after the next one is nx's (issued just now): it becomes "next"
