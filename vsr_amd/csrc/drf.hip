@@ -141,7 +141,10 @@ __global__ __launch_bounds__(256) void prelu_partial_kernel(View y, View dx, int
 __global__ __launch_bounds__(256) void slope_final_kernel(const double* __restrict__ part, int n,
                                                           const float* __restrict__ a, float* __restrict__ da,
                                                           int accumulate, int pre) {
-  constexpr int U = 4;
+  // U loads in flight per lane: a deferred DRF region is T x 4096 doubles
+  // (~1 MB at cfg 3), read by this one workgroup -- latency-bound (U = 4:
+  // 64 us per PReLU, 18 finals on the step's critical path)
+  constexpr int U = 16;
   __shared__ double sh[256];
   double s = 0.0;
   for (int base = threadIdx.x; base < n; base += 256 * U) {
