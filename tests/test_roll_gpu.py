@@ -116,6 +116,31 @@ def test_roll_tiling_invariant(case):
         assert torch.equal(y, y0), (depth, cap, (y - y0).abs().max().item())
 
 
+def test_roll_forward_sample_split():
+    """a batch whose view spans more than 2^31 elements (DUF's 256-channel
+    concat buffer at cfg 5: 128 windows) runs on the rolling kernel in sample
+    chunks (32-bit element offsets): bitwise equal to launches over each half,
+    which fit -- the conv_fast fallback it used to take accumulates in another
+    order"""
+    n, d, h, w, cw, ci, co = 80, 7, 64, 64, 1024, 64, 32
+    g = torch.Generator(device=DEV).manual_seed(3)
+    big = torch.randn((n, d, h, w, cw), generator=g, device=DEV).to(torch.bfloat16)
+    x = big[..., :ci]
+    assert (n - 1) * big.stride(0) >= 2 ** 31 > (n // 2 - 1) * big.stride(0)
+    wt = torch.randn((co, ci, 3, 3, 3), generator=g, device=DEV) / (27 * ci) ** 0.5
+    b = torch.randn(co, generator=g, device=DEV)
+    kw = dict(bias=b, prologue=F.PRO_AFFINE_RELU, pro_scale=torch.rand(ci, generator=g, device=DEV) + 0.5,
+              pro_shift=torch.randn(ci, generator=g, device=DEV) * 0.5)
+    wp = F.pack_weight(wt, 0, torch.bfloat16)
+    y = torch.empty((n, d, h, w, co), dtype=torch.bfloat16, device=DEV)
+    F.conv(x, wp, y, (3, 3, 3), (1, 1, 1), **kw)
+    for lo, hi in ((0, n // 2), (n // 2, n)):
+        yp = torch.empty((hi - lo, d, h, w, co), dtype=torch.bfloat16, device=DEV)
+        F.conv(x[lo:hi], wp, yp, (3, 3, 3), (1, 1, 1), **kw)
+        assert torch.equal(y[lo:hi], yp), (lo, (y[lo:hi].float() - yp.float()).abs().max().item())
+    del big
+
+
 def test_roll_matches_fast_path():
     """the rolling kernel and the per-kd-stage conv_fast kernel agree within
     16-bit rounding at a DUF unit shape (and the switch really changes path)"""

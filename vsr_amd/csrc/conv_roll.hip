@@ -1388,10 +1388,60 @@ void vsrk_conv_set_roll_fold_mode(int mode) { g_roll_fold_mode = mode; }
 // 1 = launched, 0 = not eligible, < 0 = -(error status)
 size_t vsrk_roll_slope_ws_bytes() { return (size_t)roll_num_cus() * RNW * sizeof(double); }
 
+static int roll_fwd_one(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
+                        const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s, const vsrk_slope_out* slope,
+                        vsrk_roll_bnred* bnred);
+
+// The rolling kernels address their views with 32-bit element offsets.  A
+// batch whose views span more (DUF's 256-channel concat buffer at cfg 5:
+// 128 windows x 7 x 128 x 128 x 256 = 3.8e9 elements) is launched in sample
+// chunks that fit, for the forms without a cross-sample reduction (the BN
+// reduce and the PReLU slope partials are per launch); before, such a
+// batch fell back to conv_fast.
 int vsrk_conv_fwd_roll(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
                        const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s, const vsrk_slope_out* slope,
                        vsrk_roll_bnred* bnred) {
+  auto span = [](const vsrk_tensor5* t, int64_t n) -> int64_t {  // as roll_fwd_one's check, for n samples
+    const int64_t r = t->shuffle > 1 ? t->shuffle : 1;
+    return (n - 1) * t->sn + (int64_t)(t->d - 1) * t->sd + (int64_t)(r * (t->h + RFTH + 2) - 1) * t->sh +
+           (int64_t)(r * (t->w + 2 * RHW) - 1) * t->sw + t->c;
+  };
+  const vsrk_tensor5* ts[4] = {x, y, residual, mask};
+  auto fits = [&](int64_t n) {
+    for (const vsrk_tensor5* t : ts)
+      if (t && span(t, n) >= (1ll << 31)) return false;
+    return true;
+  };
+  if (slope || bnred || x->n <= 1 || y->n != x->n || fits(x->n))
+    return roll_fwd_one(d, x, w_packed, bias, pro_scale, pro_shift, residual, mask, y, s, slope, bnred);
+  for (const vsrk_tensor5* t : ts)
+    if (t && (t->n != x->n || t->sn < 0)) return 0;
+  int nc = x->n;
+  while (nc > 1 && !fits(nc)) nc = (nc + 1) / 2;
+  if (!fits(nc)) return 0;
+  for (int n0 = 0; n0 < x->n; n0 += nc) {
+    vsrk_tensor5 c[4];
+    for (int i = 0; i < 4; ++i) {
+      if (!ts[i]) continue;
+      c[i] = *ts[i];
+      c[i].n = std::min(nc, x->n - n0);
+      c[i].ptr = (char*)ts[i]->ptr + (int64_t)n0 * ts[i]->sn * vsrk_esize(ts[i]->dtype);
+    }
+    const int rc = roll_fwd_one(d, &c[0], w_packed, bias, pro_scale, pro_shift, residual ? &c[2] : nullptr,
+                                mask ? &c[3] : nullptr, &c[1], s, nullptr, nullptr);
+    if (rc == 0 && n0 == 0) return 0;  // not eligible: nothing launched
+    if (rc == 0) return -VSRK_ERR_INVALID;  // (same shapes, fewer samples: cannot happen)
+    if (rc < 0) return rc;
+  }
+  return 1;
+}
+
+static int roll_fwd_one(const vsrk_conv_desc* d, const vsrk_tensor5* x, const void* w_packed, const float* bias,
+                        const float* pro_scale, const float* pro_shift, const vsrk_tensor5* residual,
+                        const vsrk_tensor5* mask, const vsrk_tensor5* y, hipStream_t s, const vsrk_slope_out* slope,
+                        vsrk_roll_bnred* bnred) {
   if (g_roll_mode < 0) {
     const char* e = getenv("VSRK_CONV_ROLL");
     g_roll_mode = !e ? 2 : (e[0] == '0' ? 0 : 1);
