@@ -141,6 +141,29 @@ def test_roll_forward_sample_split():
     del big
 
 
+def test_roll_wgrad_sample_split():
+    """the rolling weight gradient over a view spanning more than 2^31
+    elements runs in sample chunks, each reduced onto dw after the first:
+    bitwise the two half-batch calls (the second accumulating)"""
+    n, d, h, w, cw, ci, co = 80, 7, 64, 64, 1024, 64, 32
+    g = torch.Generator(device=DEV).manual_seed(4)
+    big = torch.randn((n, d, h, w, cw), generator=g, device=DEV).to(torch.bfloat16)
+    x = big[..., :ci]
+    dy = torch.randn((n, d, h, w, co), generator=g, device=DEV).to(torch.bfloat16)
+    assert (n - 1) * big.stride(0) >= 2 ** 31 > (n // 2) * big.stride(0)
+    kw = dict(prologue=F.PRO_AFFINE_RELU, pro_scale=torch.rand(ci, generator=g, device=DEV) + 0.5,
+              pro_shift=torch.randn(ci, generator=g, device=DEV) * 0.5)
+    dw = torch.empty((co, ci, 3, 3, 3), device=DEV)
+    db = torch.empty(co, device=DEV)
+    F.conv_wgrad(x, dy, (3, 3, 3), (1, 1, 1), dw, db, **kw)
+    dw2, db2 = torch.empty_like(dw), torch.empty_like(db)
+    F.conv_wgrad(x[:n // 2], dy[:n // 2], (3, 3, 3), (1, 1, 1), dw2, db2, **kw)
+    F.conv_wgrad(x[n // 2:], dy[n // 2:], (3, 3, 3), (1, 1, 1), dw2, db2, accumulate=True, **kw)
+    assert torch.equal(dw, dw2), (dw - dw2).abs().max().item()
+    assert torch.equal(db, db2), (db - db2).abs().max().item()
+    del big
+
+
 def test_roll_matches_fast_path():
     """the rolling kernel and the per-kd-stage conv_fast kernel agree within
     16-bit rounding at a DUF unit shape (and the switch really changes path)"""

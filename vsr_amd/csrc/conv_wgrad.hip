@@ -470,11 +470,35 @@ static WgradPlan wgrad_plan(const vsrk_conv_desc* d, const vsrk_tensor5* x, cons
   return p;
 }
 
+// Views spanning more than the rolling weight gradient's 32-bit element
+// offsets (DUF's concat buffer at cfg 5) run in sample chunks that fit: the
+// chunk's sample count, 0 when no split applies
+static int wgrad_roll_chunk(const vsrk_tensor5* x, const vsrk_tensor5* dy) {
+  auto fits = [&](int64_t n) {
+    for (const vsrk_tensor5* t : {x, dy})
+      if (n * t->sn + (int64_t)t->d * t->sd + (int64_t)(t->h + 64) * t->sh + (int64_t)(t->w + 64) * t->sw + t->c >=
+          (1ll << 31))
+        return false;
+    return true;
+  };
+  if (x->n <= 1 || x->n != dy->n || x->sn < 0 || dy->sn < 0 || fits(x->n)) return 0;
+  int nc = x->n;
+  while (nc > 1 && !fits(nc)) nc = (nc + 1) / 2;
+  return fits(nc) ? nc : 0;
+}
+
 extern "C" size_t vsrk_conv_wgrad_workspace_size(const vsrk_conv_desc* d, const vsrk_tensor5* x,
                                                  const vsrk_tensor5* dy) {
   int ns, tps, nt, dzc;
   size_t roll = 0;
-  if (!vsrk_wgrad_roll_plan(d, x, dy, &ns, &tps, &nt, &dzc, &roll)) roll = 0;
+  if (!vsrk_wgrad_roll_plan(d, x, dy, &ns, &tps, &nt, &dzc, &roll)) {
+    roll = 0;
+    if (const int nc = wgrad_roll_chunk(x, dy)) {  // the sample chunks' plan
+      vsrk_tensor5 xc = *x, gc = *dy;
+      xc.n = gc.n = nc;
+      if (!vsrk_wgrad_roll_plan(d, &xc, &gc, &ns, &tps, &nt, &dzc, &roll)) roll = 0;
+    }
+  }
   VsrkRowPlan rp;
   const size_t row = vsrk_wgrad_row_plan(d, x, dy, &rp) ? rp.ws_bytes : 0;
   return std::max(std::max(std::max(wgrad_plan(d, x, dy).ws_bytes, vsrk_conv_wgrad_pw_workspace(d, x, dy)), roll), row);
@@ -518,19 +542,43 @@ extern "C" int vsrk_conv_wgrad(const vsrk_conv_desc* d, const vsrk_tensor5* x, c
   if (pw != 0) return pw > 0 ? VSRK_OK : -pw;
   if (workspace && dy->n * dy->d * dy->h * dy->w > 0) {
     // rolling-depth 3x3x3 kernel (conv_wgrad_roll.hip): its slabs, the same reduce
-    int ns = 0;
-    if (vsrk_conv_wgrad_roll(d, x, dy, pro_scale, pro_shift, dbias != nullptr, (float*)workspace, workspace_bytes,
-                             &ns, s)) {
-      VSRK_LAUNCH_CHECK("conv_wgrad(roll)");
+    auto roll = [&](const vsrk_tensor5* xv, const vsrk_tensor5* gv, int32_t acc) -> bool {
+      int ns = 0;
+      if (!vsrk_conv_wgrad_roll(d, xv, gv, pro_scale, pro_shift, dbias != nullptr, (float*)workspace, workspace_bytes,
+                                &ns, s))
+        return false;
       const int nci = x->c / 32, nco = dy->c / 32;
       const int64_t total = (int64_t)dy->c * x->c * 27 + (dbias ? dy->c : 0);
       if (!wgrad_reduce_rows((const float*)workspace, dw, dbias, 2 * ns, 9 * 1024 + 32, dy->c, x->c, 3, 9, nco, nci,
-                             32, 32, std::min(d->pd, 2), perm_r, dy_scale, accumulate, s))
+                             32, 32, std::min(d->pd, 2), perm_r, dy_scale, acc, s))
         wgrad_reduce_kernel<<<(int)ceil_div64(total, 64), 256, 0, s>>>(
             (const float*)workspace, dw, dbias, 2 * ns, 3 * nci * nco, 9 * 1024 + 32, dy->c, x->c, 3, 3, 3, nco, nci,
-            32, 32, std::min(d->pd, 2), perm_r, dy_scale, accumulate);
-      VSRK_LAUNCH_CHECK("conv_wgrad_reduce");
+            32, 32, std::min(d->pd, 2), perm_r, dy_scale, acc);
+      return true;
+    };
+    if (roll(x, dy, accumulate)) {
+      VSRK_LAUNCH_CHECK("conv_wgrad(roll)");
       return VSRK_OK;
+    }
+    // views spanning more than the kernel's 32-bit element offsets (DUF's
+    // concat buffer at cfg 5): sample chunks that fit, each reduced onto dw
+    // after the first (fixed chunk order: deterministic)
+    if (const int nc = wgrad_roll_chunk(x, dy)) {
+      bool ok = true;
+      for (int n0 = 0; ok && n0 < x->n; n0 += nc) {
+        vsrk_tensor5 xc = *x, gc = *dy;
+        xc.n = gc.n = std::min(nc, x->n - n0);
+        xc.ptr = (char*)x->ptr + (int64_t)n0 * x->sn * es;
+        gc.ptr = (char*)dy->ptr + (int64_t)n0 * dy->sn * es;
+        if (!roll(&xc, &gc, n0 == 0 ? accumulate : 1)) {
+          VSRK_CHECK(n0 == 0, "conv_wgrad(roll): a sample chunk was not eligible");
+          ok = false;  // nothing launched: the other paths below
+        }
+      }
+      if (ok) {
+        VSRK_LAUNCH_CHECK("conv_wgrad(roll, sample chunks)");
+        return VSRK_OK;
+      }
     }
   }
   if (workspace && dy->n * dy->d * dy->h * dy->w > 0) {
